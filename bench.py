@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Headline benchmark: homomorphic u32 additions per second at d = d' = tau = 128, delta = 1.
+
+One step = one batched launch of the fused ripple-carry adder (src/impls/numbers/common.rs:37-56)
+over `--batch` u32 ciphertext pairs per GPU (BASELINE.json configs[1]: batch 4096), inputs
+already resident in HBM.  Multi-GPU: one process per GPU (torchrun), each rank adds its own
+shard (weak scaling, no data-path collective); keys are broadcast once over RCCL at setup and the
+decrypt-check digests are reduced after the timed region.
+
+Prints ONE JSON line (rank 0).  Besides the contract fields it carries
+  roofline      HBM roofline of the add kernel: algorithmic bytes per launch / kernel time
+  cpu_baseline  the CPU oracle (operation-for-operation restatement of the reference) timed on a
+                bounded sample on this host, single thread (the reference is single-threaded)
+  secondary     u32 encrypt+decrypt throughput (configs[2]) and u8 multiply throughput (the
+                feasible form of configs[3]; a full u32 mul is infeasible)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "homomorph-rust_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import homomorph as H  # noqa: E402
+
+PARAMS = (128, 128, 1, 128)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def make_context(world, rank, device):
+    """Keys are generated on rank 0 and broadcast to every rank (setup, untimed)."""
+    ctx = H.Context(H.Parameters(*PARAMS), device=device)
+    if rank == 0:
+        ctx.seed_rng(0xB0B)
+        ctx.generate_secret_key()
+        ctx.generate_public_key()
+    if world > 1:
+        d, dp, delta, tau = PARAMS
+        sk = torch.zeros(d // 64 + 1, dtype=torch.int64, device=device)
+        pk = torch.zeros((tau, (d + dp) // 64 + 1), dtype=torch.int64, device=device)
+        if rank == 0:
+            sk.copy_(torch.from_numpy(ctx.get_secret_key().limbs.view(np.int64)))
+            pk.copy_(torch.from_numpy(ctx.get_public_key().limbs.view(np.int64)))
+        dist.broadcast(sk, 0)
+        dist.broadcast(pk, 0)
+        if rank != 0:
+            ctx.set_secret_key(H.SecretKey(sk.cpu().numpy().view(np.uint64)))
+            ctx.set_public_key(H.PublicKey(pk.cpu().numpy().view(np.uint64)))
+    return ctx
+
+
+def time_loop(fn, steps, warmup, world):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    return wall, ev0.elapsed_time(ev1) / 1e3
+
+
+def cpu_baseline_add(seconds):
+    """Oracle (C restatement of the reference's add path) on one host core, bounded sample."""
+    from oracle import oracle_py as oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import as_bytes, fresh_bound, keys, masks
+    d, dp, delta, tau = PARAMS
+    sk, pk, _ = keys(d, dp, delta, tau, 77)
+    rng = np.random.default_rng(5)
+    n = 4
+    a = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    b = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    bound = fresh_bound(d, dp, 32)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), masks(n, 32, tau, 1), bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), masks(n, 32, tau, 2), bound)
+    ob = H.add_out_bounds(bound, bound)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        oracle.add_batch(la, da, bound, lb, db, bound, 32, n, ob)
+        done += n
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "adds/s", "cores": 1, "kind": "port",
+            "sample": f"{done} u32 homomorphic adds (4 seeded pairs, repeated) in {el:.1f} s, "
+                      f"C oracle restating src/polynomial.rs + common.rs, 1 thread, -O3"}
+
+
+def secondary_metrics(ctx, device, steps):
+    out = {}
+    # configs[2]: u32 encrypt + decrypt, batch 65536 (masks drawn on device, inputs resident)
+    n = 65536
+    tau = PARAMS[3]
+    gen = torch.Generator(device=device)
+    gen.manual_seed(7)
+    vals = torch.randint(0, 2**31, (n,), dtype=torch.int64, device=device).to(torch.int32)
+    data = vals.view(torch.uint8).reshape(n, 4)
+    m = torch.randint(0, 256, (n, 32, (tau + 7) // 8), dtype=torch.uint8, device=device, generator=gen)
+    bound = np.full(32, ctx.fresh_bound(), dtype=np.uint32)
+    c = H.Ciphered.empty(n, bound, device)
+    dec = torch.empty((n, 4), dtype=torch.uint8, device=device)
+    cb = c._c()
+    L = H.lib()
+    import ctypes
+
+    def encdec():
+        st = L.hm_encrypt_batch(ctx._h, data.data_ptr(), 4, m.data_ptr(), ctypes.byref(cb))
+        st |= L.hm_decrypt_batch(ctx._h, ctypes.byref(cb), dec.data_ptr())
+        assert st == 0
+
+    wall, _ = time_loop(encdec, steps, 2, 1)
+    ctx.synchronize()
+    ok = bool(torch.equal(dec, data))
+    out["u32_encrypt_decrypt"] = {"value": n * steps / wall, "unit": "u32 enc+dec/s",
+                                  "batch": n, "verified": ok}
+
+    # configs[3] feasible form: u8 multiply (carry-save circuit), batch 1024
+    n8 = 1024
+    a8 = np.random.default_rng(1).integers(0, 256, size=n8, dtype=np.uint8)
+    b8 = np.random.default_rng(2).integers(0, 256, size=n8, dtype=np.uint8)
+    ca, cbb = ctx.encrypt(a8), ctx.encrypt(b8)
+    ob = H.mul_out_bounds(ca.bound, cbb.bound)
+    co = H.Ciphered.empty(n8, ob, device)
+    H.mul_into(ctx, ca, cbb, co)  # sizes the workspace outside the timed loop
+    ctx.synchronize()
+    wall, _ = time_loop(lambda: H.mul_into(ctx, ca, cbb, co), max(1, steps // 4), 1, 1)
+    got = ctx.decrypt(co, np.uint8)
+    out["u8_mul"] = {"value": n8 * max(1, steps // 4) / wall, "unit": "u8 muls/s", "batch": n8,
+                     "verified": bool(np.array_equal(got, (a8.astype(int) * b8) .astype(np.uint8)))}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="u32 pairs per GPU (configs[1])")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "add_traffic.json"),
+                    help="PMC-derived HBM bytes per add launch (written by profiles/pmc.py)")
+    args = ap.parse_args()
+
+    world, rank, local = setup_dist(args.gpus)
+    device = torch.device("cuda", torch.cuda.current_device())
+    ctx = make_context(world, rank, device)
+
+    n = args.batch
+    rng = np.random.default_rng(1000 + rank)
+    a = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    b = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(31 + rank)
+    ca, cb = ctx.encrypt(a, generator=gen), ctx.encrypt(b, generator=gen)
+    ob = H.add_out_bounds(ca.bound, cb.bound)
+    out = H.Ciphered.empty(n, ob, device, np.dtype(np.uint32))
+    ctx.synchronize()
+
+    wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, args.warmup, world)
+    ctx.synchronize()  # raises on any device-side error flag
+    # verification (untimed): decrypt and compare; digests reduced over RCCL
+    dec = ctx.decrypt(out)
+    correct = torch.tensor([int(np.sum(dec == (a + b).astype(np.uint32)))], device=device)
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(correct, op=dist.ReduceOp.SUM)
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    wall = float(wall_t.item())
+    total = n * world * args.steps
+
+    in_bytes = 8 * (ca.stride + cb.stride)
+    out_bytes = 8 * out.stride
+    per_add = in_bytes + out_bytes
+    kernel_s = ev_s / args.steps
+    achieved = n * per_add / kernel_s / 1e9
+    traffic = None
+    try:
+        with open(args.traffic) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch_per_4096")
+        if traffic is not None:
+            traffic = traffic * n / 4096
+    except (OSError, ValueError):
+        traffic = None
+
+    result = {
+        "metric": "homomorphic u32 ops/sec (add, mul) at d=dp=tau=128; 1/2/4/8 MI355X",
+        "value": total / wall,
+        "unit": "u32 homomorphic adds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * wall / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (GF(2)[X] over u64 limbs)",
+        "data": "synthetic: seeded u32 plaintexts, seeded keys, device-drawn subset masks",
+        "config": {"workload": "u32 homomorphic add (configs[1])", "global_batch": n * world,
+                   "batch_per_gpu": n, "d": PARAMS[0], "dp": PARAMS[1], "delta": PARAMS[2],
+                   "tau": PARAMS[3], "parallelism": f"batch-sharded x{world}"},
+        "verified": {"correct_sums": int(correct.item()), "of": n * world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel_ms": 1e3 * kernel_s, "alg_bytes_per_add": per_add,
+                     "note": "VALU-bound carry-less arithmetic; see DESIGN.md for the VALU roofline"},
+    }
+    if rank == 0 and world == 1 and not args.no_secondary:
+        try:
+            result["secondary"] = secondary_metrics(ctx, device, max(4, args.steps // 2))
+        except Exception as e:  # reported, never fatal to the headline line
+            result["secondary"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb_ = cpu_baseline_add(args.cpu_seconds)
+        result["cpu_baseline"] = cb_
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,753 @@
+// capi.cpp — host side of the C ABI declared in include/homomorph_gpu.h.
+//
+// Owns the per-device context (keys, derived decrypt table, workspace, stream), validates every
+// call the way the reference's safe wrappers do (Context::validate_operation, src/context.rs:
+// 310-323; Parameters::new asserts, :87-94), computes static degree bounds and per-wave LDS carve-
+// outs, and launches the kernels of kernels.hip.  Never throws across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <random>
+#include <vector>
+
+#include "engine.h"
+
+using namespace hm;
+
+struct hm_ctx {
+    uint16_t d, dp, delta, tau;
+    int device;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t rng = 0;
+    // keys (host copies; SecretKey / PublicKey)
+    bool has_sk = false, has_pk = false;
+    std::vector<uint64_t> sk;          // limbs of S
+    std::vector<uint64_t> pk;          // tau * pk_cap limbs
+    uint32_t pk_tau = 0, pk_cap = 0;
+    uint32_t pk_maxdeg = 0;
+    // device state
+    uint64_t *d_pk = nullptr;
+    uint64_t *d_z = nullptr;           // decrypt parity table z_k = (X^k mod S)(0)
+    uint32_t z_limbs = 0;
+    uint64_t *d_s = nullptr;           // divisor scratch for hm_poly_rem_batch
+    size_t d_s_limbs = 0;
+    uint32_t *d_ws = nullptr;          // multiplier workspace
+    size_t ws_bytes = 0;
+    int *d_status = nullptr;
+    hipError_t last_hip = hipSuccess;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
+inline uint32_t words_of_bound(int64_t b) { return b < 0 ? 0u : (uint32_t)(b / 32 + 1); }
+
+uint64_t splitmix64(uint64_t &s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+size_t degree_of(const uint64_t *c, size_t n) {
+    for (size_t k = n; k-- > 0;)
+        if (c[k]) return 64 * k + 63 - (size_t)__builtin_clzll(c[k]);
+    return 0;
+}
+
+// Polynomial::random(degree) (src/polynomial.rs:73-96) from the context stream.
+std::vector<uint64_t> random_poly(size_t degree, uint64_t &st) {
+    std::vector<uint64_t> v(degree / 64 + 1);
+    for (auto &w : v) w = splitmix64(st);
+    v.back() &= (1ull << (degree % 64)) - 1;
+    v.back() |= 1ull << (degree % 64);
+    return v;
+}
+
+// Host carry-less product for key generation only (setup path, runs once per key).
+std::vector<uint64_t> clmul_host(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b) {
+    std::vector<uint64_t> r(a.size() + b.size(), 0);
+    for (size_t i = 0; i < a.size(); ++i) {
+        for (size_t j = 0; j < b.size(); ++j) {
+            uint64_t lo = 0, hi = 0, x = a[i], y = b[j];
+            while (x) {
+                unsigned k = (unsigned)__builtin_ctzll(x);
+                lo ^= y << k;
+                if (k) hi ^= y >> (64 - k);
+                x &= x - 1;
+            }
+            r[i + j] ^= lo;
+            r[i + j + 1] ^= hi;
+        }
+    }
+    return r;
+}
+
+hm_status hip_fail(hm_ctx *c, hipError_t e) {
+    if (c) c->last_hip = e;
+    return HM_ERR_HIP;
+}
+
+#define HM_HIP(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) return hip_fail((ctx), _e);                                         \
+    } while (0)
+
+uint16_t min_d_over_delta(hm_op op) { // src/impls/numbers.rs:27-50
+    switch (op) {
+    case HM_OP_AND: case HM_OP_OR: return 2;
+    case HM_OP_XOR: case HM_OP_NOT: return 1;
+    case HM_OP_ADD: return 21;
+    case HM_OP_MUL: case HM_OP_MUL_SIGNED: return 64;
+    }
+    return 0xFFFF;
+}
+
+bool fill_bounds(Bounds &dst, const hm_batch *b) {
+    if (!b || !b->bound || b->nbits == 0 || b->nbits > HM_MAX_BITS) return false;
+    std::memset(&dst, 0, sizeof(dst));
+    for (uint32_t i = 0; i < b->nbits; ++i) dst.b[i] = b->bound[i];
+    return true;
+}
+
+BatchArg batch_arg(const hm_batch *b) {
+    BatchArg a;
+    a.limbs = b->limbs;
+    a.degree = b->degree;
+    a.stride = hm_batch_stride(b->nbits, b->bound);
+    return a;
+}
+
+// the bound of an output must cover the computed bound, bit by bit
+bool covers(const hm_batch *out, const std::vector<uint32_t> &need) {
+    for (uint32_t i = 0; i < out->nbits; ++i)
+        if (out->bound[i] < need[i]) return false;
+    return true;
+}
+
+hm_status upload_pk(hm_ctx *c) {
+    DeviceGuard g(c->device);
+    if (c->d_pk) (void)hipFree(c->d_pk), c->d_pk = nullptr;
+    HM_HIP(c, hipMalloc(&c->d_pk, c->pk.size() * 8));
+    HM_HIP(c, hipMemcpy(c->d_pk, c->pk.data(), c->pk.size() * 8, hipMemcpyHostToDevice));
+    return HM_OK;
+}
+
+void drop_secret(hm_ctx *c) {
+    // SecretKey's Drop zeroizes (src/context.rs:197-206): zero host copy and device tables
+    if (!c->sk.empty()) {
+        volatile uint64_t *p = c->sk.data();
+        for (size_t i = 0; i < c->sk.size(); ++i) p[i] = 0;
+    }
+    c->sk.clear();
+    if (c->d_z) {
+        (void)hipMemset(c->d_z, 0, (size_t)c->z_limbs * 8);
+        (void)hipFree(c->d_z);
+        c->d_z = nullptr;
+        c->z_limbs = 0;
+    }
+    c->has_sk = false;
+}
+
+// z_k = (X^k mod S)(0) for k < 64*limbs: the decrypt functional (DESIGN.md "Decryption").
+hm_status ensure_ztable(hm_ctx *c, uint32_t max_bound) {
+    const uint32_t need = max_bound / 64 + 1;
+    if (c->d_z && c->z_limbs >= need) return HM_OK;
+    const size_t ds = degree_of(c->sk.data(), c->sk.size());
+    bool nonzero = false;
+    for (auto w : c->sk) nonzero |= (w != 0);
+    if (!nonzero) return HM_ERR_DIVIDE_BY_ZERO;
+    if (ds == 0) return HM_ERR_DIVISOR_IS_ONE;
+    const size_t sl = ds / 64 + 1;
+    std::vector<uint64_t> r(sl, 0), z(need, 0);
+    r[0] = 1; // X^0
+    for (size_t k = 0; k < (size_t)need * 64; ++k) {
+        if (r[0] & 1) z[k / 64] |= 1ull << (k % 64);
+        // r = X*r mod S  (r has degree < ds)
+        uint64_t carry = 0;
+        for (size_t w = 0; w < sl; ++w) {
+            uint64_t nc = r[w] >> 63;
+            r[w] = (r[w] << 1) | carry;
+            carry = nc;
+        }
+        if ((r[ds / 64] >> (ds % 64)) & 1)
+            for (size_t w = 0; w < sl; ++w) r[w] ^= c->sk[w];
+    }
+    DeviceGuard g(c->device);
+    if (c->d_z) {
+        (void)hipMemset(c->d_z, 0, (size_t)c->z_limbs * 8);
+        (void)hipFree(c->d_z);
+        c->d_z = nullptr;
+    }
+    HM_HIP(c, hipMalloc(&c->d_z, (size_t)need * 8));
+    HM_HIP(c, hipMemcpy(c->d_z, z.data(), (size_t)need * 8, hipMemcpyHostToDevice));
+    volatile uint64_t *pz = z.data();
+    for (size_t i = 0; i < z.size(); ++i) pz[i] = 0;
+    c->z_limbs = need;
+    return HM_OK;
+}
+
+hm_status check_batch(const hm_batch *b, bool need_limbs = true) {
+    if (!b || !b->bound || b->nbits == 0 || b->nbits > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
+    if (b->n && need_limbs && (!b->limbs || !b->degree)) return HM_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < b->nbits; ++i)
+        if (b->bound[i] > (1u << 30)) return HM_ERR_UNSUPPORTED;
+    return HM_OK;
+}
+
+} // namespace
+
+// =============================================================================================
+extern "C" {
+
+const char *hm_status_string(hm_status s) {
+    switch (s) {
+    case HM_OK: return "ok";
+    case HM_ERR_INVALID_PARAMETERS: return "invalid parameters (d < min_d_over_delta * delta)";
+    case HM_ERR_SECRET_KEY_UNSET: return "secret key unset";
+    case HM_ERR_PUBLIC_KEY_UNSET: return "public key unset";
+    case HM_ERR_DIVIDE_BY_ZERO: return "attempt to divide by zero";
+    case HM_ERR_DIVISOR_IS_ONE: return "divisor is the constant 1";
+    case HM_ERR_CAPACITY: return "output exceeds its capacity";
+    case HM_ERR_UNSUPPORTED: return "unsupported size";
+    case HM_ERR_HIP: return "HIP runtime error";
+    case HM_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case HM_ERR_INVALID_CIPHERED_LENGTH: return "ciphered length is not a multiple of 8";
+    case HM_ERR_BAD_INPUT: return "input degree does not match its limbs";
+    }
+    return "unknown status";
+}
+
+uint32_t hm_abi_version(void) { return HM_ABI_VERSION; }
+
+hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, int device,
+                        hm_ctx **out) {
+    if (!out) return HM_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (d == 0 || dp == 0 || delta == 0 || tau == 0 || delta >= d) return HM_ERR_INVALID_PARAMETERS;
+    hm_ctx *c = new (std::nothrow) hm_ctx();
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    c->d = d, c->dp = dp, c->delta = delta, c->tau = tau, c->device = device;
+    std::random_device rd; // OS randomness, as getrandom in the reference
+    c->rng = ((uint64_t)rd() << 32) ^ rd();
+    DeviceGuard g(device);
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->d_status, sizeof(int));
+    if (e == hipSuccess) e = hipMemset(c->d_status, 0, sizeof(int));
+    if (e != hipSuccess) {
+        if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return HM_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return HM_OK;
+}
+
+void hm_ctx_destroy(hm_ctx *c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    drop_secret(c);
+    if (c->d_pk) (void)hipFree(c->d_pk);
+    if (c->d_s) (void)hipFree(c->d_s);
+    if (c->d_ws) (void)hipFree(c->d_ws);
+    if (c->d_status) (void)hipFree(c->d_status);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+hm_status hm_ctx_set_stream(hm_ctx *c, void *s) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return HM_OK;
+}
+
+void *hm_ctx_stream(const hm_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+hm_status hm_ctx_parameters(const hm_ctx *c, uint16_t *d, uint16_t *dp, uint16_t *delta,
+                            uint16_t *tau) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (d) *d = c->d;
+    if (dp) *dp = c->dp;
+    if (delta) *delta = c->delta;
+    if (tau) *tau = c->tau;
+    return HM_OK;
+}
+
+hm_status hm_ctx_set_secret_key(hm_ctx *c, const uint64_t *limbs, size_t n) {
+    if (!c || !limbs || n == 0) return HM_ERR_INVALID_ARGUMENT; // from_bytes asserts non-empty
+    drop_secret(c);
+    c->sk.assign(limbs, limbs + n);
+    c->has_sk = true;
+    c->has_pk = false; // set_secret_key clears the public key (src/context.rs:568-571)
+    return HM_OK;
+}
+
+hm_status hm_ctx_set_public_key(hm_ctx *c, const uint64_t *limbs, uint32_t tau, uint32_t lpp) {
+    if (!c || !limbs || tau == 0 || lpp == 0) return HM_ERR_INVALID_ARGUMENT;
+    c->pk.assign(limbs, limbs + (size_t)tau * lpp);
+    c->pk_tau = tau, c->pk_cap = lpp;
+    c->pk_maxdeg = 0;
+    for (uint32_t i = 0; i < tau; ++i)
+        c->pk_maxdeg = std::max<uint32_t>(c->pk_maxdeg, (uint32_t)degree_of(&c->pk[(size_t)i * lpp], lpp));
+    hm_status st = upload_pk(c);
+    if (st == HM_OK) c->has_pk = true;
+    return st;
+}
+
+hm_status hm_ctx_seed_rng(hm_ctx *c, uint64_t seed) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    c->rng = seed;
+    return HM_OK;
+}
+
+hm_status hm_ctx_generate_secret_key(hm_ctx *c) { // src/context.rs:421-424
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    std::vector<uint64_t> s = random_poly(c->d, c->rng);
+    hm_status st = hm_ctx_set_secret_key(c, s.data(), s.size());
+    volatile uint64_t *p = s.data();
+    for (size_t i = 0; i < s.size(); ++i) p[i] = 0;
+    return st;
+}
+
+hm_status hm_ctx_generate_public_key(hm_ctx *c) { // src/context.rs:249-261, :444-454
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
+    const uint32_t cap = ((uint32_t)c->d + c->dp) / 64 + 1;
+    std::vector<uint64_t> all((size_t)c->tau * cap, 0);
+    for (uint32_t i = 0; i < c->tau; ++i) {
+        std::vector<uint64_t> q = random_poly(c->dp, c->rng);
+        std::vector<uint64_t> sq = clmul_host(c->sk, q);
+        std::vector<uint64_t> r = random_poly(c->delta, c->rng);
+        // X * R: shift left by one
+        std::vector<uint64_t> rx(r.size() + 1, 0);
+        for (size_t w = 0; w < r.size(); ++w) {
+            rx[w] |= r[w] << 1;
+            rx[w + 1] |= r[w] >> 63;
+        }
+        for (size_t w = 0; w < cap; ++w) {
+            uint64_t v = (w < sq.size() ? sq[w] : 0) ^ (w < rx.size() ? rx[w] : 0);
+            all[(size_t)i * cap + w] = v;
+        }
+        // anything above cap would mean deg T_i > d + dp, impossible by construction
+    }
+    return hm_ctx_set_public_key(c, all.data(), c->tau, cap);
+}
+
+hm_status hm_ctx_get_secret_key(const hm_ctx *c, uint64_t *limbs, size_t cap, size_t *n) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
+    if (n) *n = c->sk.size();
+    if (limbs) {
+        if (cap < c->sk.size()) return HM_ERR_CAPACITY;
+        std::memcpy(limbs, c->sk.data(), c->sk.size() * 8);
+    }
+    return HM_OK;
+}
+
+hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, uint32_t *tau,
+                                uint32_t *lpp) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (!c->has_pk) return HM_ERR_PUBLIC_KEY_UNSET;
+    if (tau) *tau = c->pk_tau;
+    if (lpp) *lpp = c->pk_cap;
+    if (limbs) {
+        if (cap < c->pk.size()) return HM_ERR_CAPACITY;
+        std::memcpy(limbs, c->pk.data(), c->pk.size() * 8);
+    }
+    return HM_OK;
+}
+
+hm_status hm_validate_operation(const hm_ctx *c, hm_op op, uint16_t *req) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    const uint16_t m = min_d_over_delta(op);
+    if (req) *req = m;
+    if ((uint32_t)c->d < (uint32_t)m * (uint32_t)c->delta) return HM_ERR_INVALID_PARAMETERS;
+    return HM_OK;
+}
+
+uint32_t hm_fresh_bound(const hm_ctx *c) { return c ? (uint32_t)c->d + c->dp : 0; }
+
+uint64_t hm_batch_stride(uint32_t nbits, const uint32_t *bound) {
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < nbits; ++i) s += cap_of(bound[i]);
+    return s;
+}
+
+// Degree bounds of common.rs:37-56 (deg(xy) = deg x + deg y, deg(x+y) <= max).
+hm_status hm_add_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, uint32_t *out) {
+    if (!a || !b || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
+    int64_t c = -1; // null carry
+    for (uint32_t i = 0; i < L; ++i) {
+        const int64_t x = std::max<int64_t>(a[i], b[i]);
+        const int64_t s = std::max(x, c);
+        if (s >= (int64_t)1 << 30) return HM_ERR_UNSUPPORTED;
+        out[i] = (uint32_t)s;
+        if (i + 1 < L) {
+            const int64_t ab = (int64_t)a[i] + b[i];
+            const int64_t p = x + ab;
+            c = (c < 0) ? ab : std::max(ab, p + c);
+        }
+    }
+    return HM_OK;
+}
+
+} // extern "C"
+
+namespace {
+// Symbolic run of the carry-save multiplier over degree bounds (-1 = known null).  Also reports
+// the workspace geometry the kernel needs.
+struct MulPlan {
+    std::vector<int64_t> res;
+    uint32_t kmax = 0;
+    uint32_t slot[2] = {0, 0};
+    uint32_t tmp = 0;
+    bool ok = true;
+};
+inline int64_t bmul(int64_t x, int64_t y) { return (x < 0 || y < 0) ? -1 : x + y; }
+inline int64_t bxor(int64_t x, int64_t y) { return std::max(x, y); }
+
+MulPlan plan_mul(uint32_t L, const uint32_t *a, const uint32_t *b, int is_signed) {
+    MulPlan P;
+    P.res.assign(L, -1);
+    std::vector<int64_t> prev, cur;
+    const int64_t lim = (int64_t)1 << 30;
+    for (uint32_t i = 0; i < L; ++i) {
+        cur.clear();
+        int64_t r = -1;
+        const bool push = i + 1 < L;
+        uint32_t slot = 0;
+        for (uint32_t j = 0; j <= i; ++j) {
+            int64_t pp = (int64_t)a[j] + b[i - j];
+            P.tmp = std::max<uint32_t>(P.tmp, 2 * cap_of(a[j]) + 2 * cap_of(b[i - j]) + 2);
+            if (is_signed) {
+                int fl = (j == 0 && i - j == L - 1) + (j == L - 1 && i - j == 0);
+                if (fl & 1) pp = std::max<int64_t>(pp, 0);
+            }
+            if (push) {
+                cur.push_back(bmul(pp, r));
+                slot = std::max(slot, words_of_bound(pp) + words_of_bound(r));
+            }
+            r = bxor(r, pp);
+            if (r > lim) P.ok = false;
+        }
+        for (int64_t c : prev) {
+            if (push) {
+                cur.push_back(bmul(r, c));
+                slot = std::max(slot, words_of_bound(r) + words_of_bound(c));
+            }
+            r = bxor(r, c);
+            if (r > lim) P.ok = false;
+        }
+        P.res[i] = r;
+        P.kmax = std::max<uint32_t>(P.kmax, (uint32_t)cur.size());
+        P.slot[i & 1] = std::max(P.slot[i & 1], slot + 2);
+        prev.swap(cur);
+    }
+    return P;
+}
+} // namespace
+
+extern "C" {
+
+hm_status hm_mul_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, int is_signed,
+                            uint32_t *out) {
+    if (!a || !b || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
+    MulPlan P = plan_mul(L, a, b, is_signed);
+    if (!P.ok) return HM_ERR_UNSUPPORTED;
+    for (uint32_t i = 0; i < L; ++i) out[i] = (uint32_t)std::max<int64_t>(P.res[i], 0);
+    return HM_OK;
+}
+
+hm_status hm_gate_out_bounds(hm_op g, uint32_t L, const uint32_t *a, const uint32_t *b,
+                             uint32_t *out) {
+    if (!a || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
+    if (g != HM_OP_NOT && !b) return HM_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < L; ++i) {
+        uint64_t v;
+        switch (g) {
+        case HM_OP_AND: case HM_OP_OR: v = (uint64_t)a[i] + b[i]; break;
+        case HM_OP_XOR: v = std::max(a[i], b[i]); break;
+        case HM_OP_NOT: v = a[i]; break;
+        default: return HM_ERR_INVALID_ARGUMENT;
+        }
+        if (v >= (1u << 30)) return HM_ERR_UNSUPPORTED;
+        out[i] = (uint32_t)v;
+    }
+    return HM_OK;
+}
+
+// ------------------------------------------------------------------ cipher
+hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, const uint8_t *masks,
+                           hm_batch *out) {
+    if (!c || !out) return HM_ERR_INVALID_ARGUMENT;
+    if (!c->has_pk) return HM_ERR_PUBLIC_KEY_UNSET;
+    if (hm_status st = check_batch(out); st) return st;
+    if (nbytes == 0 || out->nbits != 8 * nbytes) return HM_ERR_INVALID_ARGUMENT;
+    if (out->n && (!data || !masks)) return HM_ERR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < out->nbits; ++i)
+        if (out->bound[i] < c->pk_maxdeg) return HM_ERR_INVALID_ARGUMENT;
+    if (out->n == 0) return HM_OK;
+    EncArgs E{};
+    E.pk = c->d_pk, E.tau = c->pk_tau, E.pk_cap = c->pk_cap;
+    E.data = data, E.nbytes = nbytes, E.masks = masks;
+    E.out = batch_arg(out);
+    E.n = out->n;
+    E.status = c->d_status;
+    fill_bounds(E.ob, out);
+    DeviceGuard g(c->device);
+    int r = launch_encrypt(E, c->stream);
+    if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
+    return r ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) {
+    if (!c || !in) return HM_ERR_INVALID_ARGUMENT;
+    if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
+    if (in->nbits % 8) return HM_ERR_INVALID_CIPHERED_LENGTH; // cipher.rs:218-220
+    if (hm_status st = check_batch(in); st) return st;
+    if (in->n == 0) return HM_OK;
+    if (!out) return HM_ERR_INVALID_ARGUMENT;
+    uint32_t mb = 0;
+    for (uint32_t i = 0; i < in->nbits; ++i) mb = std::max(mb, in->bound[i]);
+    if (hm_status st = ensure_ztable(c, mb); st) return st;
+    DecArgs D{};
+    D.in = batch_arg(in);
+    D.n = in->n, D.nbits = in->nbits;
+    D.z = c->d_z, D.zlimbs = c->z_limbs;
+    D.out = out;
+    D.status = c->d_status;
+    fill_bounds(D.ib, in);
+    DeviceGuard g(c->device);
+    return launch_decrypt(D, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+// ------------------------------------------------------------------ operations
+hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch *out) {
+    if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
+    if (hm_status st = hm_validate_operation(c, HM_OP_ADD, nullptr); st) return st;
+    for (const hm_batch *x : {a, b, (const hm_batch *)out})
+        if (hm_status st = check_batch(x); st) return st;
+    if (a->nbits != b->nbits || a->nbits != out->nbits || a->n != b->n || a->n != out->n)
+        return HM_ERR_INVALID_ARGUMENT;
+    const uint32_t L = a->nbits;
+    std::vector<uint32_t> need(L);
+    if (hm_status st = hm_add_out_bounds(L, a->bound, b->bound, need.data()); st) return st;
+    if (!covers(out, need)) return HM_ERR_INVALID_ARGUMENT;
+    if (a->n == 0) return HM_OK;
+
+    // LDS plan (32-bit words per wave), simulated along the chain from the input bounds
+    uint32_t SA = 0, SB = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        SA = std::max(SA, 2 * cap_of(a->bound[i]));
+        SB = std::max(SB, 2 * cap_of(b->bound[i]));
+    }
+    const uint32_t SX = std::max(SA, SB), SAB = SA + SB, SP = SX + SAB;
+    uint32_t SC = 2;
+    int64_t cb = -1;
+    for (uint32_t i = 0; i + 1 < L; ++i) {
+        const int64_t x = std::max<int64_t>(a->bound[i], b->bound[i]);
+        const int64_t ab = (int64_t)a->bound[i] + b->bound[i];
+        const int64_t p = x + ab;
+        const uint32_t need_w = std::max(words_of_bound(p) + words_of_bound(cb), words_of_bound(ab));
+        SC = std::max(SC, need_w + 2);
+        cb = (cb < 0) ? ab : std::max(ab, p + cb);
+    }
+    auto even = [](uint32_t v) { return (v + 3) & ~1u; };
+    AddArgs A{};
+    uint32_t o = 0;
+    A.lds.oA = o, o += even(SA);
+    A.lds.oB = o, o += even(SB);
+    A.lds.oX = o, o += even(SX);
+    A.lds.oAB = o, o += even(SAB);
+    A.lds.oP = o, o += even(SP);
+    A.lds.oC0 = o, o += even(SC);
+    A.lds.oC1 = o, o += even(SC);
+    A.lds.per_wave = o;
+    A.lds.max_prod_words = std::max(SC, std::max(SP, SAB));
+    if ((size_t)o * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
+    A.a = batch_arg(a), A.b = batch_arg(b), A.out = batch_arg(out);
+    A.n = a->n, A.nbits = L;
+    A.status = c->d_status;
+    fill_bounds(A.ab, a), fill_bounds(A.bb, b), fill_bounds(A.ob, out);
+    DeviceGuard g(c->device);
+    return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,
+                       hm_batch *out) {
+    if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
+    if (hm_status st = hm_validate_operation(c, is_signed ? HM_OP_MUL_SIGNED : HM_OP_MUL, nullptr); st)
+        return st;
+    for (const hm_batch *x : {a, b, (const hm_batch *)out})
+        if (hm_status st = check_batch(x); st) return st;
+    if (a->nbits != b->nbits || a->nbits != out->nbits || a->n != b->n || a->n != out->n)
+        return HM_ERR_INVALID_ARGUMENT;
+    const uint32_t L = a->nbits;
+    MulPlan P = plan_mul(L, a->bound, b->bound, is_signed);
+    if (!P.ok) return HM_ERR_UNSUPPORTED;
+    for (uint32_t i = 0; i < L; ++i)
+        if (out->bound[i] < (uint32_t)std::max<int64_t>(P.res[i], 0)) return HM_ERR_INVALID_ARGUMENT;
+    if (a->n == 0) return HM_OK;
+    MulArgs M{};
+    uint64_t o = 0;
+    M.oIn = 0;
+    uint64_t wa = 2 * hm_batch_stride(L, a->bound), wb = 2 * hm_batch_stride(L, b->bound);
+    M.in_words_a = (uint32_t)wa;
+    o = wa + wb;
+    for (uint32_t i = 0; i < L; ++i) {
+        M.oRes[i] = (uint32_t)o;
+        o += words_of_bound(P.res[i]) + 2;
+    }
+    M.oTmp = (uint32_t)o, o += P.tmp;
+    M.car_slot[0] = P.slot[0], M.car_slot[1] = P.slot[1];
+    M.oCar[0] = (uint32_t)o, o += (uint64_t)P.kmax * P.slot[0];
+    M.oCar[1] = (uint32_t)o, o += (uint64_t)P.kmax * P.slot[1];
+    o = (o + 63) & ~(uint64_t)63;
+    if (o >= (1ull << 32)) return HM_ERR_UNSUPPORTED;
+    M.ws_stride = o;
+    M.kmax = P.kmax;
+    M.lds_ints = 2 * L + 2 * P.kmax + 2;
+    const size_t bytes = (size_t)o * 4 * a->n;
+    DeviceGuard g(c->device);
+    if (bytes > c->ws_bytes) {
+        HM_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->d_ws) (void)hipFree(c->d_ws), c->d_ws = nullptr, c->ws_bytes = 0;
+        HM_HIP(c, hipMalloc(&c->d_ws, bytes));
+        c->ws_bytes = bytes;
+    }
+    M.ws = c->d_ws;
+    M.a = batch_arg(a), M.b = batch_arg(b), M.out = batch_arg(out);
+    M.n = a->n, M.nbits = L, M.is_signed = is_signed;
+    M.status = c->d_status;
+    fill_bounds(M.ab, a), fill_bounds(M.bb, b), fill_bounds(M.ob, out);
+    const uint32_t wpb = 4;
+    return launch_mul(M, wpb, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_gate_batch(hm_ctx *c, hm_op gate, const hm_batch *a, const hm_batch *b,
+                        hm_batch *out) {
+    if (!c || !a || !out) return HM_ERR_INVALID_ARGUMENT;
+    if (gate > HM_OP_NOT) return HM_ERR_INVALID_ARGUMENT;
+    if (hm_status st = hm_validate_operation(c, gate, nullptr); st) return st;
+    if (hm_status st = check_batch(a); st) return st;
+    if (hm_status st = check_batch(out); st) return st;
+    if (gate != HM_OP_NOT) {
+        if (!b) return HM_ERR_INVALID_ARGUMENT;
+        if (hm_status st = check_batch(b); st) return st;
+        if (b->nbits != a->nbits || b->n != a->n) return HM_ERR_INVALID_ARGUMENT;
+    }
+    if (out->nbits != a->nbits || out->n != a->n) return HM_ERR_INVALID_ARGUMENT;
+    const uint32_t L = a->nbits;
+    std::vector<uint32_t> need(L);
+    if (hm_status st = hm_gate_out_bounds(gate, L, a->bound, gate == HM_OP_NOT ? nullptr : b->bound,
+                                          need.data());
+        st)
+        return st;
+    if (!covers(out, need)) return HM_ERR_INVALID_ARGUMENT;
+    if (a->n == 0) return HM_OK;
+    uint32_t SA = 0, SB = 2;
+    for (uint32_t i = 0; i < L; ++i) {
+        SA = std::max(SA, 2 * cap_of(a->bound[i]));
+        if (gate != HM_OP_NOT) SB = std::max(SB, 2 * cap_of(b->bound[i]));
+    }
+    GateArgs G{};
+    G.op = gate;
+    G.oA = 0, G.oB = SA + 2, G.oT = G.oB + SB + 2;
+    G.lds_per_wave = G.oT + 2 * (SA + SB) + 8;
+    if ((size_t)G.lds_per_wave * 16 > 160 * 1024) return HM_ERR_UNSUPPORTED;
+    G.a = batch_arg(a);
+    if (gate != HM_OP_NOT) G.b = batch_arg(b);
+    G.out = batch_arg(out);
+    G.n = a->n, G.nbits = L;
+    G.status = c->d_status;
+    fill_bounds(G.ab, a);
+    if (gate != HM_OP_NOT) fill_bounds(G.bb, b);
+    fill_bounds(G.ob, out);
+    DeviceGuard g(c->device);
+    return launch_gate(G, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+// ------------------------------------------------------------------ polynomial primitives
+static PolyArgs poly_args(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) {
+    PolyArgs P{};
+    P.a = a->limbs, P.adeg = a->degree, P.acap = a->cap;
+    if (b) P.b = b->limbs, P.bdeg = b->degree, P.bcap = b->cap;
+    P.out = out->limbs, P.odeg = out->degree, P.ocap = out->cap;
+    P.n = a->n;
+    P.status = c->d_status;
+    return P;
+}
+
+hm_status hm_poly_add_batch(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) {
+    if (!c || !a || !b || !out || a->n != b->n || a->n != out->n) return HM_ERR_INVALID_ARGUMENT;
+    if (!a->cap || !b->cap || out->cap < std::max(a->cap, b->cap)) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    return launch_poly_add(poly_args(c, a, b, out), c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_poly_mul_batch(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) {
+    if (!c || !a || !b || !out || a->n != b->n || a->n != out->n) return HM_ERR_INVALID_ARGUMENT;
+    if (!a->cap || !b->cap || out->cap < a->cap + b->cap) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    return launch_poly_mul(poly_args(c, a, b, out), c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, size_t sn,
+                            hm_polys *out) {
+    if (!c || !a || !out || !s || sn == 0 || a->n != out->n) return HM_ERR_INVALID_ARGUMENT;
+    if (!a->cap || out->cap < a->cap) return HM_ERR_INVALID_ARGUMENT;
+    bool nz = false;
+    for (size_t i = 0; i < sn; ++i) nz |= s[i] != 0;
+    if (!nz) return HM_ERR_DIVIDE_BY_ZERO;           // polynomial.rs:319-322
+    const size_t ds = degree_of(s, sn);
+    if (ds == 0) return HM_ERR_DIVISOR_IS_ONE;       // the reference never terminates
+    const size_t sl = ds / 64 + 1;
+    DeviceGuard g(c->device);
+    if (c->d_s_limbs < sl) {
+        HM_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->d_s) (void)hipFree(c->d_s);
+        HM_HIP(c, hipMalloc(&c->d_s, sl * 8));
+        c->d_s_limbs = sl;
+    }
+    HM_HIP(c, hipMemcpyAsync(c->d_s, s, sl * 8, hipMemcpyHostToDevice, c->stream));
+    HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer may be released after return
+    return launch_poly_rem(poly_args(c, a, nullptr, out), c->d_s, (uint32_t)ds, c->stream)
+               ? hip_fail(c, hipGetLastError())
+               : HM_OK;
+}
+
+hm_status hm_ctx_synchronize(hm_ctx *c) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    int st = 0;
+    HM_HIP(c, hipMemcpy(&st, c->d_status, sizeof(int), hipMemcpyDeviceToHost));
+    if (st) HM_HIP(c, hipMemset(c->d_status, 0, sizeof(int)));
+    if (c->last_hip != hipSuccess) {
+        c->last_hip = hipSuccess;
+        return HM_ERR_HIP;
+    }
+    return (hm_status)st;
+}
+
+} // extern "C"

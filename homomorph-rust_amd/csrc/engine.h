@@ -1,0 +1,116 @@
+// engine.h — argument blocks shared by the HIP kernels (kernels.hip) and the C-ABI host code
+// (capi.cpp).  Plain structs passed to kernels by value.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/homomorph_gpu.h"
+
+namespace hm {
+
+// Per-bit-position degree bounds of a batch (cap = bound/64 + 1 limbs).  Passed by value; kernels
+// derive limb offsets with a running prefix sum.
+struct Bounds {
+    uint32_t b[HM_MAX_BITS];
+};
+
+struct BatchArg {
+    uint64_t *limbs;
+    uint32_t *degree;
+    uint64_t stride; // limbs per value
+};
+
+// Per-wave LDS carve-out of the fused adder (units: 32-bit words, all offsets even).
+struct AddLds {
+    uint32_t per_wave; // words per wave
+    uint32_t oA, oB, oX, oAB, oP, oC0, oC1;
+    uint32_t max_prod_words; // largest product output (words) along the chain
+};
+
+struct AddArgs {
+    BatchArg a, b, out;
+    uint64_t n;
+    uint32_t nbits;
+    AddLds lds;
+    int *status;
+    Bounds ab, bb, ob;
+};
+
+struct EncArgs {
+    const uint64_t *pk; // tau * pk_cap limbs
+    uint32_t tau, pk_cap;
+    const uint8_t *data;
+    uint32_t nbytes;
+    const uint8_t *masks;
+    BatchArg out;
+    uint64_t n;
+    int *status;
+    Bounds ob;
+};
+
+struct DecArgs {
+    BatchArg in;
+    uint64_t n;
+    uint32_t nbits;
+    const uint64_t *z; // z_k = (X^k mod S)(0), bit-packed, zlimbs limbs
+    uint32_t zlimbs;
+    uint8_t *out;
+    int *status;
+    Bounds ib;
+};
+
+// Gates and the carry-save multiplier keep their intermediates in a per-value global workspace.
+struct GateArgs {
+    int op;
+    BatchArg a, b, out;
+    uint64_t n;
+    uint32_t nbits;
+    uint32_t lds_per_wave, oA, oB, oT;
+    int *status;
+    Bounds ab, bb, ob;
+};
+
+struct MulArgs {
+    BatchArg a, b, out;
+    uint64_t n;
+    uint32_t nbits;
+    int is_signed;
+    uint32_t *ws;        // workspace, ws_stride words per value
+    uint64_t ws_stride;
+    uint32_t oIn, in_words_a;   // inputs a then b (words) at ws + oIn
+    uint32_t oRes[HM_MAX_BITS]; // word offsets of result columns
+    uint32_t oTmp;              // partial-product scratch
+    uint32_t oCar[2];           // two carry lists (column parity)
+    uint32_t car_slot[2];       // words per carry slot in each list
+    uint32_t kmax;              // max carries pushed by one column
+    uint32_t lds_ints;          // per-wave LDS ints: 2*nbits + 2*kmax + 1
+    int *status;
+    Bounds ab, bb, ob;
+};
+
+struct PolyArgs {
+    const uint64_t *a;
+    const uint32_t *adeg;
+    uint32_t acap;
+    const uint64_t *b;
+    const uint32_t *bdeg;
+    uint32_t bcap;
+    uint64_t *out;
+    uint32_t *odeg;
+    uint32_t ocap;
+    uint64_t n;
+    int *status;
+};
+
+// host-side launchers (kernels.hip)
+int launch_add(const AddArgs &a, void *stream);
+int launch_encrypt(const EncArgs &a, void *stream);
+int launch_decrypt(const DecArgs &a, void *stream);
+int launch_gate(const GateArgs &a, void *stream);
+int launch_mul(const MulArgs &a, uint32_t waves_per_block, void *stream);
+int launch_poly_add(const PolyArgs &a, void *stream);
+int launch_poly_mul(const PolyArgs &a, void *stream);
+int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
+
+constexpr int kAddWavesPerBlock = 4;
+
+} // namespace hm

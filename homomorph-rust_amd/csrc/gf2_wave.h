@@ -1,0 +1,203 @@
+// gf2_wave.h — wave-level GF(2)[X] primitives for gfx950 (CDNA4, wave64).
+//
+// A polynomial here is a little-endian array of 32-bit words: coefficient of X^k is bit k%32 of
+// word k/32 (the same bit order as the reference's u64 limbs, src/polynomial.rs:142-150, read as
+// two u32 halves).  One wavefront owns one polynomial operation; its 64 lanes split the OUTPUT
+// words: in a tile starting at word `base`, lane l owns words base + l*W ... base + l*W + W-1.
+//
+// Carry-less product (replaces Polynomial::mul, src/polynomial.rs:252-310).  gfx950 has no
+// carry-less multiply instruction, and MFMA is the wrong tool for XOR/AND work, so the product is
+// built from VALU funnel shifts and XORs with one operand made WAVE-UNIFORM:
+//     out = sum_q sum_r [bit r of U_q] * X^(32q + r) * V
+//         = Horner over r:  t = X*t + S_r,   S_r = sum_{q : bit r of U_q} X^(32q) V
+// U's words live in SGPRs (readfirstlane), so "is bit r of U_q set" is a scalar branch, and the
+// word shift X^(32q) V is a compile-time register index into a per-lane window `cx` of V.  Per
+// set bit of U a lane does W XORs; per Horner step W funnel shifts (v_alignbit_b32) plus one DPP
+// wave_shr:1 that carries the top bit across lanes.  That is ~0.5 VALU op per (set bit, word) —
+// about 2x fewer than the reference-style bit-serial shift-XOR (2 ops per set bit and word).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hm {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// The lane index through a volatile asm: values derived from it cannot be hoisted out of the
+// kernel's outer loops.  Without this, LICM precomputes the per-lane addresses of every inlined
+// tile width at kernel entry and keeps ~170 VGPRs live for the whole kernel.
+__device__ __forceinline__ int lane_id_local() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// lane l receives lane l-1's value; lane 0 receives `old`
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138 /*wave_shr:1*/, 0xf, 0xf,
+                                                 false);
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        int w = __shfl_xor(v, o, 64);
+        v = v > w ? v : w;
+    }
+    return (int)rfl((uint32_t)v); // uniform: keeps every size derived from it in SGPRs
+}
+
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+    return rfl(v);
+}
+
+__device__ __forceinline__ int nwords(int deg) { return (deg >> 5) + 1; }
+
+// Exact degree of a polynomial whose words are distributed in ascending lane order (lane l's
+// words all precede lane l+1's).  ldeg = the lane's highest set bit index or -1.  Returns -1 for
+// null.
+__device__ __forceinline__ int wave_top_ordered(int ldeg) {
+    uint64_t m = __ballot(ldeg >= 0);
+    if (m == 0) return -1;
+    int hl = 63 - __builtin_clzll(m);
+    return __builtin_amdgcn_readlane(ldeg, hl);
+}
+
+// One output tile of  Dst = Add ^ U*V.
+//  U  : nu uniform-operand words (any address space; read with wave-uniform addresses)
+//  V  : nv words, read per lane with bounds checks (no halo needed)
+//  Add: nadd words XORed into the result (may be nullptr with nadd = 0)
+//  tile covers output words [base, base + 64*W) ∩ [0, nout)
+// MULTI: the tile does not start at word 0, so lane 0 tracks word base-1 to shift its top bit in.
+// Returns the tile's highest set bit index (global), or -1.
+template <int W, int QC, bool MULTI>
+__device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
+                                        const uint32_t *__restrict__ V, int nv,
+                                        const uint32_t *__restrict__ Add, int nadd,
+                                        uint32_t *__restrict__ Dst, int nout, int base) {
+    // sizes are wave-uniform; say so, so every size test below is a scalar branch
+    nu = (int)rfl((uint32_t)nu), nv = (int)rfl((uint32_t)nv), nadd = (int)rfl((uint32_t)nadd);
+    nout = (int)rfl((uint32_t)nout), base = (int)rfl((uint32_t)base);
+    const int lane = lane_id_local();
+    const int w0 = base + lane * W;
+    uint32_t acc[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc[j] = (w0 + j < nadd) ? Add[w0 + j] : 0u;
+
+    const int tile_end = base + kWave * W; // exclusive
+    for (int q0 = 0; q0 < nu; q0 += QC) {
+        // U chunk words [q0, q0+QC) reach output words [q0, q0 + QC + nv)
+        if (q0 >= tile_end || base >= q0 + QC + nv) continue;
+        // window: cx[k] = V[w0 - q0 - QC + k], k in [0, W+QC)
+        uint32_t cx[W + QC];
+        const int cb = w0 - q0 - QC;
+#pragma unroll
+        for (int k = 0; k < W + QC; ++k) {
+            const int idx = cb + k;
+            cx[k] = (idx >= 0 && idx < nv) ? V[idx] : 0u;
+        }
+        uint32_t u[QC];
+#pragma unroll
+        for (int q = 0; q < QC; ++q) u[q] = (q0 + q < nu) ? rfl(U[q0 + q]) : 0u;
+
+        uint32_t t[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) t[j] = 0u;
+        uint32_t tlo = 0u; // word base-1 (lane 0 only meaningful), MULTI only
+        for (int r = 31; r >= 0; --r) {
+            // t <<= 1 across the whole distributed polynomial
+            const uint32_t prev = wave_shr1(t[W - 1], MULTI ? tlo : 0u);
+#pragma unroll
+            for (int j = W - 1; j >= 1; --j) t[j] = funnel(t[j], t[j - 1], 31);
+            t[0] = funnel(t[0], prev, 31);
+            if (MULTI) tlo <<= 1;
+#pragma unroll
+            for (int q = 0; q < QC; ++q) {
+                if ((u[q] >> r) & 1u) {
+                    asm volatile("" ::);
+#pragma unroll
+                    for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC];
+                    if (MULTI) tlo ^= cx[QC - 1 - q];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc[j] ^= t[j];
+    }
+    int ldeg = -1;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        if (w0 + j < nout) {
+            Dst[w0 + j] = acc[j];
+            if (acc[j]) ldeg = (w0 + j) * 32 + 31 - __builtin_clz(acc[j]);
+        }
+    }
+    return wave_top_ordered(ldeg);
+}
+
+template <int QC, int W, int WMAX>
+__device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32_t *V, int nv,
+                                         const uint32_t *Add, int nadd, uint32_t *Dst, int nout) {
+    int top = mul_tile<W, QC, false>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
+    if constexpr (W == WMAX) { // only the widest tile ever needs more than one pass
+        for (int base = kWave * W; base < nout; base += kWave * W) {
+            int t = mul_tile<W, QC, true>(U, nu, V, nv, Add, nadd, Dst, nout, base);
+            if (t >= 0) top = t;
+        }
+    }
+    return top;
+}
+
+// Dst[0..nout) = Add ^ U*V with nout = max(nu+nv, nadd).  Returns the exact degree (-1 = null).
+// Dst must not alias U, V or Add.  The per-lane tile width W is picked from nout among the
+// instantiated widths <= WMAX (the kernel's VGPR budget is set by WMAX + QC); longer outputs are
+// produced in several WMAX-wide tiles.
+template <int QC, int WMAX>
+__device__ __forceinline__ int wave_mul(const uint32_t *U, int nu, const uint32_t *V, int nv,
+                                        const uint32_t *Add, int nadd, uint32_t *Dst,
+                                        int *nout_p) {
+    nu = (int)rfl((uint32_t)nu), nv = (int)rfl((uint32_t)nv), nadd = (int)rfl((uint32_t)nadd);
+    const int nout = max(nu + nv, nadd);
+    *nout_p = nout;
+    const int w = (nout + kWave - 1) / kWave;
+#define HM_TRY_W(WW)                                                                              \
+    if constexpr (WW < WMAX) {                                                                    \
+        if (w <= WW) return mul_tiles<QC, WW, WMAX>(U, nu, V, nv, Add, nadd, Dst, nout);          \
+    }
+    HM_TRY_W(1)
+    HM_TRY_W(2)
+    HM_TRY_W(3)
+    HM_TRY_W(4)
+    HM_TRY_W(6)
+    HM_TRY_W(8)
+    HM_TRY_W(10)
+    HM_TRY_W(12)
+    HM_TRY_W(16)
+#undef HM_TRY_W
+    return mul_tiles<QC, WMAX, WMAX>(U, nu, V, nv, Add, nadd, Dst, nout);
+}
+
+// Dst[0..n) = A ^ B (n = max(na, nb)); exact degree (-1 = null).  Strided lane loop.
+__device__ __forceinline__ int wave_xor(const uint32_t *A, int na, const uint32_t *B, int nb,
+                                        uint32_t *Dst) {
+    const int n = max(na, nb);
+    int ldeg = -1;
+    for (int w = lane_id(); w < n; w += kWave) {
+        uint32_t v = (w < na ? A[w] : 0u) ^ (w < nb ? B[w] : 0u);
+        Dst[w] = v;
+        if (v) ldeg = w * 32 + 31 - __builtin_clz(v);
+    }
+    return wave_max_i32(ldeg);
+}
+
+} // namespace hm

@@ -1,0 +1,574 @@
+// kernels.hip — gfx950 kernels of the GF(2)[X] homomorphic engine.
+//
+//   add_kernel      fused ripple-carry adder, one wavefront per value, carry chain kept in LDS
+//                   (src/impls/numbers/common.rs:37-56 add_internal)
+//   mul_kernel      carry-save multiplier, one wavefront per value, carries in a global workspace
+//                   (common.rs:66-105 mul_unsigned_internal, :115-155 mul_signed_internal)
+//   gate_kernel     elementwise AND/OR/XOR/NOT (common.rs:5-35)
+//   encrypt_kernel  subset-sum of the public key, one lane per ciphertext bit (cipher.rs:99-115)
+//   decrypt_kernel  (C mod S)(0) as the parity functional  sum_k c_k z_k, z_k = (X^k mod S)(0):
+//                   a linear map, so it equals the reference's long-division remainder evaluated
+//                   at 0 (cipher.rs:119-122, polynomial.rs:316-365); one wavefront per value
+//   poly_* kernels  single-polynomial primitives for unit parity (polynomial.rs:190-365)
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "gf2_wave.h"
+
+namespace hm {
+
+__device__ __forceinline__ void flag(int *status, int code) {
+    if (status) atomicCAS(status, 0, code);
+}
+
+// Make this wave's LDS / global writes visible to its own later reads by other lanes, and keep
+// the compiler from reordering memory operations across the point.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
+
+// Load one ciphertext bit (u64 limbs, exact degree `deg`) into 32-bit words at dst.
+// The degree word is validated against the limbs (top bit set, nothing above it).
+// Returns the word count (0 for the null polynomial).
+__device__ int load_bit(const uint64_t *__restrict__ src, uint32_t deg, uint32_t bound,
+                        uint32_t *__restrict__ dst, int *status) {
+    const int lane = lane_id();
+    if (deg > bound) {
+        if (lane == 0) flag(status, HM_ERR_BAD_INPUT);
+        return 0;
+    }
+    const int nl = (int)(deg / 64) + 1;
+    const int cap = (int)(bound / 64) + 1;
+    const uint32_t tb = deg % 64;
+    bool bad = false;
+    for (int g = lane; g < cap; g += kWave) {
+        uint64_t v = src[g];
+        if (g >= nl) { // limbs above the degree must be zero (layout invariant)
+            bad |= v != 0;
+            continue;
+        }
+        if (g == nl - 1) {
+            const uint64_t keep = (~0ull) >> (63 - tb);
+            bad |= (v & ~keep) != 0;
+            v &= keep;
+            if (deg > 0 && !((v >> tb) & 1ull)) bad = true;
+        }
+        dst[2 * g] = (uint32_t)v;
+        dst[2 * g + 1] = (uint32_t)(v >> 32);
+    }
+    if (__any(bad) && lane == 0) flag(status, HM_ERR_BAD_INPUT);
+    if (deg == 0) {
+        const uint32_t w0 = rfl((uint32_t)src[0]);
+        if (!(w0 & 1u)) return 0;
+    }
+    return (int)(deg / 32) + 1;
+}
+
+// dst (cap limbs) = X ^ C; writes the exact degree; returns it (-1 = null).
+__device__ int store_xor_bit(const uint32_t *X, int nx, const uint32_t *C, int nc,
+                             uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
+                             int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int n = max(nx, nc);
+    const int total = max(cap, (n + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        uint32_t lo = (w < nx ? X[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        uint32_t hi = (w + 1 < nx ? X[w + 1] : 0u) ^ (w + 1 < nc ? C[w + 1] : 0u);
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+__device__ __forceinline__ int words_of(int deg) { return deg >= 0 ? nwords(deg) : 0; }
+
+// Small products (fresh operands: 9 words at d+dp = 256) use a short uniform chunk; the carry
+// product P * carry uses a chunk that covers P (25 words at d+dp = 256) in one pass.
+constexpr int kQSmall = 10;
+constexpr int kQBig = 25;
+
+// ---------------------------------------------------------------------------------------------
+// Fused ripple-carry adder.  Per bit i (common.rs:43-53):
+//   x = a_i ^ b_i;  s_i = x ^ carry;
+//   carry' = (x & carry) ^ (a_i & b_i) & ((x & carry) ^ 1)
+//          = ab ^ P * carry  with  ab = a_i b_i,  P = x (1 ^ ab)            (GF(2)[X] ring identity)
+// so each bit costs two small products (ab, x*ab) and ONE large product P * carry instead of the
+// reference's three large ones.  The carry stays in LDS for the whole chain.
+template <int WMAX>
+__global__ void __launch_bounds__(256) add_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    uint32_t *L = lds + (size_t)wave * A.lds.per_wave;
+    uint32_t *Ab = L + A.lds.oA, *Bb = L + A.lds.oB, *X = L + A.lds.oX, *AB = L + A.lds.oAB;
+    uint32_t *P = L + A.lds.oP, *C = L + A.lds.oC0, *Cn = L + A.lds.oC1;
+    const uint64_t *pa = A.a.limbs + e * A.a.stride;
+    const uint64_t *pb = A.b.limbs + e * A.b.stride;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    const uint32_t *da = A.a.degree + e * A.nbits;
+    const uint32_t *db = A.b.degree + e * A.nbits;
+    uint32_t *dout = A.out.degree + e * A.nbits;
+
+    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    uint32_t offa = 0, offb = 0, offo = 0;
+    for (uint32_t i = 0; i < A.nbits; ++i) {
+        const uint32_t dga = rfl(da[i]), dgb = rfl(db[i]);
+        const int na = load_bit(pa + offa, dga, A.ab.b[i], Ab, A.status);
+        const int nb = load_bit(pb + offb, dgb, A.bb.b[i], Bb, A.status);
+        wsync();
+        const int nx = words_of(wave_xor(Ab, na, Bb, nb, X));
+        wsync();
+        store_xor_bit(X, nx, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
+        if (i + 1 < A.nbits) {
+            int nout;
+            const int nab = words_of(wave_mul<kQSmall, WMAX>(Ab, na, Bb, nb, nullptr, 0, AB, &nout));
+            wsync();
+            const int np = words_of(wave_mul<kQSmall, WMAX>(X, nx, AB, nab, X, nx, P, &nout));
+            wsync();
+            nc = words_of(wave_mul<kQBig, WMAX>(P, np, C, nc, AB, nab, Cn, &nout));
+            wsync();
+            uint32_t *t = C;
+            C = Cn;
+            Cn = t;
+        }
+        offa += cap_of(A.ab.b[i]);
+        offb += cap_of(A.bb.b[i]);
+        offo += cap_of(A.ob.b[i]);
+    }
+    (void)lane;
+}
+
+int launch_add(const AddArgs &a, void *stream) {
+    const int wpb = kAddWavesPerBlock;
+    const uint64_t blocks = (a.n + wpb - 1) / wpb;
+    if (blocks == 0) return 0;
+    const size_t lds = (size_t)a.lds.per_wave * 4 * wpb;
+    // the widest per-lane tile the carry chain needs (carry + P words over 64 lanes)
+    const uint32_t need = (a.lds.max_prod_words + 63) / 64;
+    if (need <= 4)
+        hipLaunchKernelGGL(add_kernel<4>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
+    else if (need <= 8)
+        hipLaunchKernelGGL(add_kernel<8>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
+    else if (need <= 12)
+        hipLaunchKernelGGL(add_kernel<12>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
+    else if (need <= 16)
+        hipLaunchKernelGGL(add_kernel<16>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(add_kernel<24>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Elementwise gates: one wavefront per value, bit by bit through LDS.
+//   AND = a*b, XOR = a+b, OR = a+b+ab, NOT = a+1    (cipher.rs:58-90)
+__global__ void __launch_bounds__(256) gate_kernel(GateArgs G) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= G.n) return;
+    const int lane = lane_id();
+    uint32_t *L = lds + (size_t)wave * G.lds_per_wave;
+    uint32_t *Ab = L + G.oA, *Bb = L + G.oB, *T = L + G.oT;
+    const uint64_t *pa = G.a.limbs + e * G.a.stride;
+    const uint64_t *pb = G.op == HM_OP_NOT ? nullptr : G.b.limbs + e * G.b.stride;
+    uint64_t *po = G.out.limbs + e * G.out.stride;
+    uint32_t offa = 0, offb = 0, offo = 0;
+    for (uint32_t i = 0; i < G.nbits; ++i) {
+        const int na = load_bit(pa + offa, rfl(G.a.degree[e * G.nbits + i]), G.ab.b[i], Ab, G.status);
+        int nb = 0;
+        if (G.op == HM_OP_NOT) {
+            if (lane == 0) Bb[0] = 1u; // the unit polynomial, CipheredBit::one (cipher.rs:49-51)
+            nb = 1;
+        } else {
+            nb = load_bit(pb + offb, rfl(G.b.degree[e * G.nbits + i]), G.bb.b[i], Bb, G.status);
+        }
+        wsync();
+        int nt = 0, nout;
+        const uint32_t *R = T;
+        if (G.op == HM_OP_AND) {
+            nt = words_of(wave_mul<kQSmall, 8>(Ab, na, Bb, nb, nullptr, 0, T, &nout));
+        } else if (G.op == HM_OP_OR) {
+            // a + b + ab: first X = a ^ b into T's tail, then T = X ^ a*b
+            uint32_t *Xs = T + (na + nb + 2);
+            const int nx = words_of(wave_xor(Ab, na, Bb, nb, Xs));
+            wsync();
+            nt = words_of(wave_mul<kQSmall, 8>(Ab, na, Bb, nb, Xs, nx, T, &nout));
+        } else { // XOR, NOT
+            nt = words_of(wave_xor(Ab, na, Bb, nb, T));
+        }
+        wsync();
+        store_xor_bit(R, nt, nullptr, 0, po + offo, G.ob.b[i], G.out.degree + e * G.nbits + i,
+                      G.status);
+        wsync();
+        offa += cap_of(G.ab.b[i]);
+        if (G.op != HM_OP_NOT) offb += cap_of(G.bb.b[i]);
+        offo += cap_of(G.ob.b[i]);
+    }
+}
+
+int launch_gate(const GateArgs &g, void *stream) {
+    const int wpb = 4;
+    const uint64_t blocks = (g.n + wpb - 1) / wpb;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(gate_kernel, dim3((unsigned)blocks), dim3(64 * wpb),
+                       (size_t)g.lds_per_wave * 4 * wpb, (hipStream_t)stream, g);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Carry-save multiplier (common.rs:66-105; signed variant :115-155 flips pp[0][L-1], pp[L-1][0]).
+// Column i: for j <= i: pp = a_j b_{i-j}; push(pp * res_i); res_i ^= pp;
+//           for every carry c of column i-1: push(res_i * c); res_i ^= c.
+// Carries are not pushed in the last column.  Partial products that no column consumes
+// (j + k >= L) are never formed: they cannot affect any output.
+// All polynomials live in the value's global workspace (L2 resident); one wavefront per value.
+__device__ int ws_xor_into(uint32_t *R, int nr, const uint32_t *B, int nb) {
+    // R ^= B in place, returns the new exact degree (-1 = null)
+    const int n = max(nr, nb);
+    int ldeg = -1;
+    for (int w = lane_id(); w < n; w += kWave) {
+        uint32_t v = (w < nr ? R[w] : 0u) ^ (w < nb ? B[w] : 0u);
+        R[w] = v;
+        if (v) ldeg = w * 32 + 31 - __builtin_clz(v);
+    }
+    return wave_max_i32(ldeg);
+}
+
+__global__ void __launch_bounds__(256) mul_kernel(MulArgs M) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const int wpb = blockDim.x >> 6;
+    const uint64_t e = (uint64_t)blockIdx.x * wpb + wave;
+    if (e >= M.n) return;
+    const int lane = lane_id();
+    const uint32_t L = M.nbits;
+    // per-wave LDS: word counts of a/b bits and of the two carry lists, plus the unit polynomial
+    int *meta = (int *)lds + (size_t)wave * M.lds_ints;
+    int *na = meta, *nb = meta + L, *cw0 = meta + 2 * L, *cw1 = cw0 + M.kmax;
+    uint32_t *one = (uint32_t *)(cw1 + M.kmax);
+    if (lane == 0) one[0] = 1u;
+    uint32_t *ws = M.ws + e * M.ws_stride;
+    uint32_t *Ain = ws + M.oIn, *Bin = ws + M.oIn + M.in_words_a;
+    // load inputs (validated, masked) into the workspace
+    {
+        const uint64_t *pa = M.a.limbs + e * M.a.stride, *pb = M.b.limbs + e * M.b.stride;
+        uint32_t oa = 0, ob = 0;
+        for (uint32_t i = 0; i < L; ++i) {
+            int x = load_bit(pa + oa, rfl(M.a.degree[e * L + i]), M.ab.b[i], Ain + 2 * oa, M.status);
+            int y = load_bit(pb + ob, rfl(M.b.degree[e * L + i]), M.bb.b[i], Bin + 2 * ob, M.status);
+            if (lane == 0) na[i] = x, nb[i] = y;
+            oa += cap_of(M.ab.b[i]);
+            ob += cap_of(M.bb.b[i]);
+        }
+    }
+    wsync();
+    uint32_t *Tmp = ws + M.oTmp;
+    uint32_t offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        uint32_t *R = ws + M.oRes[i];
+        int nr = 0;
+        const int cur = i & 1;
+        int *cwc = cur ? cw1 : cw0, *cwp = cur ? cw0 : cw1;
+        uint32_t *Cc = ws + M.oCar[cur], *Cp = ws + M.oCar[cur ^ 1];
+        const uint32_t sc = M.car_slot[cur], sp = M.car_slot[cur ^ 1];
+        const bool push = i + 1 < L;
+        int k = 0, nout;
+        for (uint32_t j = 0; j <= i; ++j) {
+            // pp = a_j * b_{i-j}   (signed: pp[0][L-1] and pp[L-1][0] get ^1, common.rs:123-126)
+            uint32_t oa = 0, ob = 0;
+            for (uint32_t t = 0; t < j; ++t) oa += cap_of(M.ab.b[t]);
+            for (uint32_t t = 0; t < i - j; ++t) ob += cap_of(M.bb.b[t]);
+            int flips = 0;
+            if (M.is_signed) flips = (j == 0 && i - j == L - 1) + (j == L - 1 && i - j == 0);
+            const int xa = rfl(na[j]), xb = rfl(nb[i - j]);
+            const int np = words_of(wave_mul<kQBig, 8>(Ain + 2 * oa, xa, Bin + 2 * ob, xb,
+                                                    (flips & 1) ? one : nullptr, flips & 1, Tmp,
+                                                    &nout));
+            wsync();
+            if (push) {
+                // carries.push(pp & result[i])  (common.rs:83-87): the smaller operand is uniform
+                int c;
+                if (np <= nr) c = wave_mul<kQBig, 8>(Tmp, np, R, nr, nullptr, 0, Cc + k * sc, &nout);
+                else c = wave_mul<kQBig, 8>(R, nr, Tmp, np, nullptr, 0, Cc + k * sc, &nout);
+                if ((uint32_t)nout > sc) flag(M.status, HM_ERR_CAPACITY);
+                if (lane == 0) cwc[k] = words_of(c);
+                ++k;
+                wsync();
+            }
+            nr = words_of(ws_xor_into(R, nr, Tmp, np));
+            wsync();
+        }
+        const int cur_len = (int)(i * (i + 1) / 2);
+        for (int j = 0; j < cur_len; ++j) {
+            const uint32_t *Cj = Cp + (size_t)j * sp;
+            const int ncj = rfl(cwp[j]);
+            if (push) {
+                int c;
+                if (ncj <= nr) c = wave_mul<kQBig, 8>(Cj, ncj, R, nr, nullptr, 0, Cc + k * sc, &nout);
+                else c = wave_mul<kQBig, 8>(R, nr, Cj, ncj, nullptr, 0, Cc + k * sc, &nout);
+                if ((uint32_t)nout > sc) flag(M.status, HM_ERR_CAPACITY);
+                if (lane == 0) cwc[k] = words_of(c);
+                ++k;
+                wsync();
+            }
+            nr = words_of(ws_xor_into(R, nr, Cj, ncj));
+            wsync();
+        }
+        store_xor_bit(R, nr, nullptr, 0, M.out.limbs + e * M.out.stride + offo, M.ob.b[i],
+                      M.out.degree + e * L + i, M.status);
+        offo += cap_of(M.ob.b[i]);
+        wsync();
+    }
+}
+
+int launch_mul(const MulArgs &m, uint32_t wpb, void *stream) {
+    const uint64_t blocks = (m.n + wpb - 1) / wpb;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(mul_kernel, dim3((unsigned)blocks), dim3(64 * wpb),
+                       (size_t)m.lds_ints * 4 * wpb, (hipStream_t)stream, m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Encryption: one lane per ciphertext bit.  C = XOR_{i : mask bit i} T_i, then C ^= x
+// (CipheredBit::cipher, cipher.rs:99-115; Ciphered::try_cipher bit order :180-185).  The public
+// key T_i is read with wave-uniform addresses (scalar loads); the mask select is one bitop3
+// (acc ^ (t & m)) per 32-bit half.
+template <int PC>
+__global__ void __launch_bounds__(256) encrypt_kernel(EncArgs E) {
+    const uint32_t nbits = E.nbytes * 8;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= E.n * nbits) return;
+    const uint64_t e = t / nbits;
+    const uint32_t k = (uint32_t)(t % nbits);
+    const uint32_t mb = (E.tau + 7) / 8;
+    const uint8_t *m = E.masks + t * mb;
+    uint32_t lo[PC], hi[PC];
+#pragma unroll
+    for (int l = 0; l < PC; ++l) lo[l] = hi[l] = 0u;
+    for (uint32_t i0 = 0; i0 < E.tau; i0 += 32) {
+        uint32_t bits;
+        if ((mb & 3u) == 0) {
+            bits = *(const uint32_t *)(m + i0 / 8);
+        } else {
+            bits = 0;
+            for (uint32_t b = 0; b < 4 && i0 / 8 + b < mb; ++b) bits |= (uint32_t)m[i0 / 8 + b] << (8 * b);
+        }
+        const uint32_t cnt = min(32u, E.tau - i0);
+        for (uint32_t ii = 0; ii < cnt; ++ii) {
+            const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)bits, ii, 1); // 0 or ~0
+            const uint32_t *pk = (const uint32_t *)(E.pk + (size_t)(i0 + ii) * PC);
+#pragma unroll
+            for (int l = 0; l < PC; ++l) {
+                lo[l] = __builtin_amdgcn_bitop3_b32(lo[l], pk[2 * l], msk, 0x6a);     // lo ^ (pk & m)
+                hi[l] = __builtin_amdgcn_bitop3_b32(hi[l], pk[2 * l + 1], msk, 0x6a);
+            }
+        }
+    }
+    lo[0] ^= (E.data[e * E.nbytes + k / 8] >> (k % 8)) & 1u; // add_bool_assign (:112)
+    uint32_t off = 0;
+    for (uint32_t j = 0; j < k; ++j) off += cap_of(E.ob.b[j]);
+    const uint32_t cap = cap_of(E.ob.b[k]);
+    uint64_t *dst = E.out.limbs + e * E.out.stride + off;
+    int deg = 0;
+#pragma unroll
+    for (int l = 0; l < PC; ++l) {
+        const uint64_t v = (uint64_t)lo[l] | ((uint64_t)hi[l] << 32);
+        if (v) deg = l * 64 + 63 - __builtin_clzll(v);
+        if ((uint32_t)l < cap) dst[l] = v;
+        else if (v) flag(E.status, HM_ERR_CAPACITY);
+    }
+    for (uint32_t l = PC; l < cap; ++l) dst[l] = 0ull;
+    if ((uint32_t)deg > E.ob.b[k]) flag(E.status, HM_ERR_CAPACITY);
+    E.out.degree[e * nbits + k] = (uint32_t)deg;
+}
+
+template <int PC>
+static void launch_enc_pc(const EncArgs &E, void *stream) {
+    const uint64_t threads = E.n * E.nbytes * 8;
+    const uint64_t blocks = (threads + 255) / 256;
+    hipLaunchKernelGGL(encrypt_kernel<PC>, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, E);
+}
+
+int launch_encrypt(const EncArgs &E, void *stream) {
+    if (E.n == 0) return 0;
+    switch (E.pk_cap) {
+    case 1: launch_enc_pc<1>(E, stream); break;
+    case 2: launch_enc_pc<2>(E, stream); break;
+    case 3: launch_enc_pc<3>(E, stream); break;
+    case 4: launch_enc_pc<4>(E, stream); break;
+    case 5: launch_enc_pc<5>(E, stream); break;
+    case 6: launch_enc_pc<6>(E, stream); break;
+    case 7: launch_enc_pc<7>(E, stream); break;
+    case 8: launch_enc_pc<8>(E, stream); break;
+    case 9: launch_enc_pc<9>(E, stream); break;
+    case 10: launch_enc_pc<10>(E, stream); break;
+    case 11: launch_enc_pc<11>(E, stream); break;
+    case 12: launch_enc_pc<12>(E, stream); break;
+    case 13: launch_enc_pc<13>(E, stream); break;
+    case 14: launch_enc_pc<14>(E, stream); break;
+    case 15: launch_enc_pc<15>(E, stream); break;
+    case 16: launch_enc_pc<16>(E, stream); break;
+    case 17: launch_enc_pc<17>(E, stream); break;
+    default: return HM_ERR_UNSUPPORTED;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decryption: bit = parity(C & z) with z_k = (X^k mod S)(0).  One wavefront per value; lanes
+// stride over the value's limbs (coalesced), accumulate per-bit parities, XOR-reduce.
+__global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
+    __shared__ uint32_t offs[HM_MAX_BITS + 1];
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (uint32_t i = 0; i < D.nbits; ++i) offs[i] = s, s += cap_of(D.ib.b[i]);
+        offs[D.nbits] = s;
+    }
+    __syncthreads();
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= D.n) return;
+    const int lane = lane_id();
+    const uint64_t *src = D.in.limbs + e * D.in.stride;
+    const uint32_t total = offs[D.nbits];
+    uint64_t m0 = 0, m1 = 0;
+    uint32_t i = 0;
+    bool bad = false;
+    for (uint32_t g = lane; g < total; g += kWave) {
+        while (g >= offs[i + 1]) ++i;
+        const uint64_t v = src[g];
+        const uint32_t zi = g - offs[i];
+        uint64_t z = 0;
+        if (zi < D.zlimbs) z = D.z[zi];
+        else if (v) bad = true;
+        const uint64_t p = (uint64_t)(__builtin_popcountll(v & z) & 1);
+        if (i < 64) m0 ^= p << i;
+        else m1 ^= p << (i - 64);
+    }
+    if (__any(bad) && lane == 0) flag(D.status, HM_ERR_UNSUPPORTED);
+    const uint32_t r0 = wave_xor_u32((uint32_t)m0), r1 = wave_xor_u32((uint32_t)(m0 >> 32));
+    const uint32_t r2 = wave_xor_u32((uint32_t)m1), r3 = wave_xor_u32((uint32_t)(m1 >> 32));
+    const uint32_t nbytes = D.nbits / 8;
+    if ((uint32_t)lane < nbytes) {
+        const uint32_t w = lane / 4;
+        const uint32_t word = w == 0 ? r0 : w == 1 ? r1 : w == 2 ? r2 : r3;
+        D.out[e * nbytes + lane] = (uint8_t)(word >> (8 * (lane % 4)));
+    }
+}
+
+int launch_decrypt(const DecArgs &D, void *stream) {
+    if (D.n == 0) return 0;
+    const uint64_t blocks = (D.n + 3) / 4;
+    hipLaunchKernelGGL(decrypt_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, D);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Single-polynomial primitives (unit parity for polynomial.rs).  Inputs must satisfy the layout
+// invariant (bits above the degree are zero); word views of the u64 limbs are used directly.
+__device__ __forceinline__ int poly_words(const uint64_t *limbs, uint32_t deg) {
+    if (deg == 0 && (rfl((uint32_t)limbs[0]) & 1u) == 0) return 0;
+    return nwords((int)deg);
+}
+
+__device__ void zero_tail_and_degree(uint64_t *out, uint32_t ocap, int deg, uint32_t *odeg,
+                                     int written_words) {
+    uint32_t *w = (uint32_t *)out;
+    for (int k = written_words + lane_id(); k < (int)(2 * ocap); k += kWave) w[k] = 0u;
+    if (lane_id() == 0) *odeg = (uint32_t)max(deg, 0);
+}
+
+__global__ void __launch_bounds__(256) poly_add_kernel(PolyArgs P) {
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (e >= P.n) return;
+    const uint64_t *a = P.a + e * P.acap, *b = P.b + e * P.bcap;
+    uint64_t *o = P.out + e * P.ocap;
+    const int na = poly_words(a, rfl(P.adeg[e])), nb = poly_words(b, rfl(P.bdeg[e]));
+    const int deg = wave_xor((const uint32_t *)a, na, (const uint32_t *)b, nb, (uint32_t *)o);
+    zero_tail_and_degree(o, P.ocap, deg, P.odeg + e, max(na, nb));
+}
+
+__global__ void __launch_bounds__(256) poly_mul_kernel(PolyArgs P) {
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (e >= P.n) return;
+    const uint64_t *a = P.a + e * P.acap, *b = P.b + e * P.bcap;
+    uint64_t *o = P.out + e * P.ocap;
+    const int na = poly_words(a, rfl(P.adeg[e])), nb = poly_words(b, rfl(P.bdeg[e]));
+    int nout;
+    int deg;
+    if (na <= nb)
+        deg = wave_mul<kQBig, 8>((const uint32_t *)a, na, (const uint32_t *)b, nb, nullptr, 0,
+                              (uint32_t *)o, &nout);
+    else
+        deg = wave_mul<kQBig, 8>((const uint32_t *)b, nb, (const uint32_t *)a, na, nullptr, 0,
+                              (uint32_t *)o, &nout);
+    wsync();
+    zero_tail_and_degree(o, P.ocap, deg, P.odeg + e, nout);
+}
+
+// Remainder by one divisor S: thread per polynomial, bitwise long division in place on the output
+// (polynomial.rs:316-365: XOR S << (r_deg - deg S) while r_deg >= deg S).
+__global__ void __launch_bounds__(256) poly_rem_kernel(PolyArgs P, const uint64_t *S, uint32_t sdeg) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.n) return;
+    const uint64_t *a = P.a + e * P.acap;
+    uint64_t *r = P.out + e * P.ocap;
+    const uint32_t deg_a = P.adeg[e];
+    for (uint32_t k = 0; k < P.ocap; ++k) r[k] = k < P.acap ? a[k] : 0ull;
+    const uint32_t sl = sdeg / 64 + 1;
+    int rd = (int)deg_a;
+    while (rd >= (int)sdeg) {
+        if ((r[rd / 64] >> (rd % 64)) & 1ull) {
+            const uint32_t sh = (uint32_t)rd - sdeg, ws = sh / 64, bs = sh % 64;
+            for (uint32_t k = 0; k < sl; ++k) {
+                r[ws + k] ^= S[k] << bs;
+                if (bs && ws + k + 1 < P.ocap) r[ws + k + 1] ^= S[k] >> (64 - bs);
+            }
+        }
+        --rd;
+    }
+    // exact degree of the remainder (< sdeg)
+    int d = 0;
+    for (int k = (int)min(P.ocap, sl) - 1; k >= 0; --k) {
+        if (r[k]) { d = k * 64 + 63 - __builtin_clzll(r[k]); break; }
+    }
+    P.odeg[e] = (uint32_t)d;
+}
+
+int launch_poly_add(const PolyArgs &P, void *stream) {
+    if (!P.n) return 0;
+    hipLaunchKernelGGL(poly_add_kernel, dim3((unsigned)((P.n + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_poly_mul(const PolyArgs &P, void *stream) {
+    if (!P.n) return 0;
+    hipLaunchKernelGGL(poly_mul_kernel, dim3((unsigned)((P.n + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_poly_rem(const PolyArgs &P, const uint64_t *S, uint32_t sdeg, void *stream) {
+    if (!P.n) return 0;
+    hipLaunchKernelGGL(poly_rem_kernel, dim3((unsigned)((P.n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, P, S, sdeg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace hm

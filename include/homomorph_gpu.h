@@ -1,0 +1,197 @@
+/*
+ * homomorph_gpu.h — C ABI of the MI355X (gfx950) GF(2)[X] homomorphic engine.
+ *
+ * This is the drop-in boundary for mathisbot/homomorph-rust's data-parallel hot path.  Each entry
+ * point names the reference item it replaces (file:line, paths relative to the reference crate).
+ * The reference has no batch API; every batch entry applies the reference's per-value operation
+ * independently to n values (one `Ciphered<T>` = nbits ciphertext bits per value).
+ *
+ * Conventions
+ *  - Plain C: pointers + sizes, no C++ types, no exceptions cross this boundary.  Every function
+ *    returns hm_status; HM_OK == 0.
+ *  - Device buffers are caller-owned device pointers (hipMalloc'd or a torch tensor's data_ptr);
+ *    the library never frees caller memory.  Launches are asynchronous on the context's stream;
+ *    no entry below synchronises unless its comment says so.
+ *  - Polynomial layout (GF(2)[X], src/polynomial.rs:23-26): coefficient of X^k is bit k%64 of
+ *    little-endian u64 limb k/64 (the code's layout, polynomial.rs:142-150, :168-173 — the doc
+ *    comment at :16-21 describing reversed bits does not match the code).  Limbs above the degree
+ *    are zero.  Degrees are exact; the null polynomial has degree 0 (polynomial.rs:126-137).
+ *  - Batch layout (hm_batch): value e, bit i occupies cap[i] = bound[i]/64 + 1 limbs at limb offset
+ *    e*stride + off[i] (off = exclusive prefix sum of cap, stride = sum(cap)); its exact degree is
+ *    degree[e*nbits + i].  bound[i] is a static degree bound for bit position i (a fresh ciphertext
+ *    has bound d+dp); outputs are sized with hm_*_out_bounds.  Bit i is bit i of the bincode fixint
+ *    little-endian image of the value (src/cipher.rs:6-13, :175-191).
+ *  - Thread-safety: calls on one context are serialised by the caller; contexts on different
+ *    devices are independent (the reference's Context is a plain value, src/context.rs:300-306).
+ */
+#ifndef HOMOMORPH_GPU_H
+#define HOMOMORPH_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HM_ABI_VERSION 1
+#define HM_MAX_BITS 128 /* u128 is the widest type with impls (src/impls/numbers/uint.rs:58) */
+
+typedef enum hm_status {
+    HM_OK = 0,
+    /* OperationError::InvalidParameters (src/operations.rs:11-18) */
+    HM_ERR_INVALID_PARAMETERS = 1,
+    /* ContextCryptoError::SecretKeyUnset / PublicKeyUnset (src/context.rs:41-46) */
+    HM_ERR_SECRET_KEY_UNSET = 2,
+    HM_ERR_PUBLIC_KEY_UNSET = 3,
+    /* Polynomial::rem panics "attempt to divide by zero" (src/polynomial.rs:319-322) */
+    HM_ERR_DIVIDE_BY_ZERO = 4,
+    /* Polynomial::rem by the constant 1 never terminates in the reference (:330-343) */
+    HM_ERR_DIVISOR_IS_ONE = 5,
+    /* an output would exceed the capacity its bound gives (device-side check) */
+    HM_ERR_CAPACITY = 6,
+    /* sizes beyond what this build's kernels handle */
+    HM_ERR_UNSUPPORTED = 7,
+    HM_ERR_HIP = 8,
+    HM_ERR_INVALID_ARGUMENT = 9,
+    /* CipherError::InvalidCipheredLength (src/cipher.rs:18-24, :218-220) */
+    HM_ERR_INVALID_CIPHERED_LENGTH = 10,
+    /* an input polynomial's degree word disagrees with its limbs (device-side check) */
+    HM_ERR_BAD_INPUT = 11,
+} hm_status;
+
+/* Operation marker types and their OperationRequirement::MIN_D_OVER_DELTA
+ * (src/impls/numbers.rs:9-50). */
+typedef enum hm_op {
+    HM_OP_AND = 0,            /* HomomorphicAndGate,        min d/delta 2  */
+    HM_OP_OR = 1,             /* HomomorphicOrGate,         min d/delta 2  */
+    HM_OP_XOR = 2,            /* HomomorphicXorGate,        min d/delta 1  */
+    HM_OP_NOT = 3,            /* HomomorphicNotGate,        min d/delta 1  */
+    HM_OP_ADD = 4,            /* HomomorphicAddition,       min d/delta 21 */
+    HM_OP_MUL = 5,            /* HomomorphicMultiplication, min d/delta 64 (unsigned types) */
+    HM_OP_MUL_SIGNED = 6,     /* HomomorphicMultiplication on i8..i128 (common.rs:115-163) */
+} hm_op;
+
+typedef struct hm_ctx hm_ctx;
+
+/* A batch of n values of nbits ciphertext bits each, in device memory (layout above). */
+typedef struct hm_batch {
+    uint64_t *limbs;        /* device, n*stride limbs */
+    uint32_t *degree;       /* device, n*nbits exact degrees */
+    const uint32_t *bound;  /* HOST, nbits per-bit-position degree bounds */
+    uint32_t nbits;         /* 1..HM_MAX_BITS */
+    uint64_t n;             /* number of values */
+} hm_batch;
+
+/* A batch of n independent polynomials, each with cap limbs, in device memory. */
+typedef struct hm_polys {
+    uint64_t *limbs;        /* device, n*cap limbs */
+    uint32_t *degree;       /* device, n exact degrees */
+    uint32_t cap;           /* limbs per polynomial */
+    uint64_t n;
+} hm_polys;
+
+/* ---------------- library / context ---------------- */
+const char *hm_status_string(hm_status s);
+uint32_t hm_abi_version(void);
+
+/* Context::new(Parameters::new(d, dp, delta, tau)) — src/context.rs:345-351 with the asserts of
+ * Parameters::new (:87-94: all > 0, delta < d) reported as HM_ERR_INVALID_PARAMETERS.
+ * device: HIP device ordinal; the context creates its own non-blocking stream. */
+hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, int device,
+                        hm_ctx **out);
+/* Drop: device copies of the secret key (and tables derived from it) are zeroed before release,
+ * mirroring SecretKey's Drop (src/context.rs:197-206). */
+void hm_ctx_destroy(hm_ctx *ctx);
+/* Use a caller stream (hipStream_t passed as void*) instead of the context's own; NULL restores. */
+hm_status hm_ctx_set_stream(hm_ctx *ctx, void *hip_stream);
+void *hm_ctx_stream(const hm_ctx *ctx);
+/* Parameters getters (src/context.rs:96-118). */
+hm_status hm_ctx_parameters(const hm_ctx *ctx, uint16_t *d, uint16_t *dp, uint16_t *delta,
+                            uint16_t *tau);
+
+/* Context::set_secret_key(SecretKey::from_bytes) — src/context.rs:568-571 + :153-155.  limbs: host
+ * little-endian u64 limbs of S (the bytes of SecretKey::to_bytes).  Clears the public key, as the
+ * reference does. */
+hm_status hm_ctx_set_secret_key(hm_ctx *ctx, const uint64_t *limbs, size_t nlimbs);
+/* Context::set_public_key(PublicKey::from_bytes) — src/context.rs:593-595 + :239-245.  limbs: host,
+ * tau polynomials of limbs_per_poly limbs each (row-major). */
+hm_status hm_ctx_set_public_key(hm_ctx *ctx, const uint64_t *limbs, uint32_t tau,
+                                uint32_t limbs_per_poly);
+/* Context::generate_secret_key / generate_public_key — src/context.rs:421-454 (keygen shape
+ * S = random(d), T_i = S*Q_i + X*R_i, :160-162 and :249-261).  The reference draws from
+ * getrandom; here both draw from the context's SplitMix64 stream (DESIGN.md "RNG contract"),
+ * seeded from the OS at creation or explicitly with hm_ctx_seed_rng for reproducible keys.
+ * generate_secret_key clears the public key (:421-424); generate_public_key needs the secret key
+ * (HM_ERR_SECRET_KEY_UNSET otherwise, :444-454). */
+hm_status hm_ctx_seed_rng(hm_ctx *ctx, uint64_t seed);
+hm_status hm_ctx_generate_secret_key(hm_ctx *ctx);
+hm_status hm_ctx_generate_public_key(hm_ctx *ctx);
+/* Key export (SecretKey::to_bytes :192-194 / PublicKey::to_bytes :291-297) into host buffers. */
+hm_status hm_ctx_get_secret_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, size_t *nlimbs);
+hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, uint32_t *tau,
+                                uint32_t *limbs_per_poly);
+
+/* Context::validate_operation (src/context.rs:310-323): HM_OK or HM_ERR_INVALID_PARAMETERS with
+ * the OperationError payload written to *required_min_d_over_delta (may be NULL). */
+hm_status hm_validate_operation(const hm_ctx *ctx, hm_op op, uint16_t *required_min_d_over_delta);
+
+/* Static degree bounds (host only, no device work).  fresh bound = d + dp. */
+uint32_t hm_fresh_bound(const hm_ctx *ctx);
+/* Output bounds of the ripple-carry adder (common.rs:37-56) for input bounds a,b (nbits each). */
+hm_status hm_add_out_bounds(uint32_t nbits, const uint32_t *a_bound, const uint32_t *b_bound,
+                            uint32_t *out_bound);
+/* Output bounds of the carry-save multiplier (common.rs:66-105 / :115-155). */
+hm_status hm_mul_out_bounds(uint32_t nbits, const uint32_t *a_bound, const uint32_t *b_bound,
+                            int is_signed, uint32_t *out_bound);
+/* Output bounds of a gate (common.rs:5-35). */
+hm_status hm_gate_out_bounds(hm_op gate, uint32_t nbits, const uint32_t *a_bound,
+                             const uint32_t *b_bound, uint32_t *out_bound);
+/* stride (limbs per value) of a batch with these bounds */
+uint64_t hm_batch_stride(uint32_t nbits, const uint32_t *bound);
+
+/* ---------------- cipher (src/cipher.rs) ---------------- */
+/* Context::encrypt over a batch — Ciphered::try_cipher (cipher.rs:175-191) and
+ * CipheredBit::cipher (:99-115).  data: device, n*nbytes plaintext bytes (the bincode fixint LE
+ * image of each value).  masks: device, n*(8*nbytes)*ceil(tau/8) bytes; bit k of value e uses the
+ * ceil(tau/8) bytes at ((e*8*nbytes)+k)*ceil(tau/8), mask bit i = byte[i/8] >> (i%8) & 1 — exactly
+ * the bytes CipheredBit::part (:92-97) draws from getrandom.  out: nbits = 8*nbytes, every bound
+ * >= hm_fresh_bound.  Requires the public key. */
+hm_status hm_encrypt_batch(hm_ctx *ctx, const uint8_t *data, uint32_t nbytes,
+                           const uint8_t *masks, hm_batch *out);
+/* Context::decrypt over a batch — Ciphered::try_decipher (cipher.rs:217-250): bit k =
+ * (C_k mod S)(0) (CipheredBit::decipher :119-122), bytes assembled LSB-first.  out: device,
+ * n*(nbits/8) bytes.  nbits % 8 != 0 -> HM_ERR_INVALID_CIPHERED_LENGTH.  Requires the secret key;
+ * the first call for a given maximum bound builds a per-key table on the host (synchronous). */
+hm_status hm_decrypt_batch(hm_ctx *ctx, const hm_batch *in, uint8_t *out);
+
+/* ---------------- operations (HomomorphicOperation2 impls, src/impls/numbers/uint.rs) ------ */
+/* Context::apply2::<HomomorphicAddition, uN>: validate (d >= 21*delta) then common::add
+ * (common.rs:37-64) per value.  a, b, out: same nbits; out bounds from hm_add_out_bounds. */
+hm_status hm_add_batch(hm_ctx *ctx, const hm_batch *a, const hm_batch *b, hm_batch *out);
+/* Context::apply2::<HomomorphicMultiplication, uN / iN> (common.rs:66-163) per value.  Needs a
+ * device workspace for the carry list; the context grows it on demand (synchronous allocation
+ * on first use per size).  Sizes beyond the engine's limits return HM_ERR_UNSUPPORTED. */
+hm_status hm_mul_batch(hm_ctx *ctx, const hm_batch *a, const hm_batch *b, int is_signed,
+                       hm_batch *out);
+/* Context::apply2::<HomomorphicAnd/Or/XorGate> and apply1::<HomomorphicNotGate> (common.rs:5-35,
+ * uint.rs:8-58).  For HM_OP_NOT, b is ignored (may be NULL). */
+hm_status hm_gate_batch(hm_ctx *ctx, hm_op gate, const hm_batch *a, const hm_batch *b,
+                        hm_batch *out);
+
+/* ---------------- polynomial primitives (src/polynomial.rs), for unit parity ---------------- */
+hm_status hm_poly_add_batch(hm_ctx *ctx, const hm_polys *a, const hm_polys *b, hm_polys *out);
+hm_status hm_poly_mul_batch(hm_ctx *ctx, const hm_polys *a, const hm_polys *b, hm_polys *out);
+/* remainder by ONE divisor s (host limbs) for every polynomial of a */
+hm_status hm_poly_rem_batch(hm_ctx *ctx, const hm_polys *a, const uint64_t *s_limbs,
+                            size_t s_nlimbs, hm_polys *out);
+
+/* ---------------- status / sync ---------------- */
+/* Waits for the context's stream, then returns (and clears) the first device-side error raised by
+ * any kernel since the last check (HM_ERR_CAPACITY, HM_ERR_BAD_INPUT) or a HIP error. */
+hm_status hm_ctx_synchronize(hm_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HOMOMORPH_GPU_H */

@@ -1,0 +1,313 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle, bit-exact.
+
+Every test feeds identical seeded keys, masks and plaintexts to both sides and compares exact
+degrees and every limb (src/polynomial.rs:417-426 equality; limbs above the degree are zero on
+both sides).  Sizes are those the oracle finishes in seconds; the full-size configurations are
+covered by size-independent properties in test_gpu_properties.py.
+"""
+import numpy as np
+import pytest
+
+from helpers import as_bytes, assert_batches_equal, fresh_bound, keys, masks, plain
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import homomorph
+    homomorph.lib()  # loud failure if the engine is not built
+    return homomorph
+
+
+def make_ctx(H, params, seed):
+    ctx = H.Context(H.Parameters(*params))
+    ctx.seed_rng(seed)
+    ctx.generate_secret_key()
+    ctx.generate_public_key()
+    return ctx
+
+
+# ------------------------------------------------------------------ polynomial primitives
+def _rand_polys(rng, n, cap, maxdeg=None):
+    out = np.zeros((n, cap), dtype=np.uint64)
+    for i in range(n):
+        deg = int(rng.integers(0, 64 * cap)) if maxdeg is None else int(rng.integers(0, maxdeg + 1))
+        kind = rng.integers(0, 8)
+        if kind == 0:
+            continue  # null polynomial
+        if kind == 1:
+            out[i, 0] = 1  # the unit
+            continue
+        nl = deg // 64 + 1
+        out[i, :nl] = rng.integers(0, 2**64, size=nl, dtype=np.uint64)
+        out[i, nl - 1] &= np.uint64((1 << (deg % 64)) - 1) if deg % 64 else np.uint64(0)
+        out[i, nl - 1] |= np.uint64(1 << (deg % 64))
+    return out
+
+
+@pytest.mark.parametrize("ca,cb", [(1, 1), (5, 5), (3, 17), (40, 2), (200, 9), (400, 400)])
+def test_poly_mul_add(H, oracle, ca, cb):
+    import torch
+    rng = np.random.default_rng(ca * 1000 + cb)
+    n = 64
+    A, B = _rand_polys(rng, n, ca), _rand_polys(rng, n, cb)
+    ctx = make_ctx(H, (64, 64, 1, 64), 1)
+    dev = ctx.device
+    pa, pb = H.Polys.from_host(A, dev), H.Polys.from_host(B, dev)
+    pm = ctx.poly_mul(pa, pb)
+    ps = ctx.poly_add(pa, pb)
+    ctx.synchronize()
+    ml, md = pm.to_host()
+    sl, sd = ps.to_host()
+    for i in range(n):
+        ref, rdeg = oracle.poly_mul(A[i], B[i])
+        assert md[i] == rdeg, (i, md[i], rdeg)
+        w = min(len(ref), ml.shape[1])
+        assert np.array_equal(ml[i, :w], ref[:w]) and not ml[i, w:].any()
+        ref, rdeg = oracle.poly_add(A[i], B[i])
+        assert sd[i] == rdeg
+        w = min(len(ref), sl.shape[1])
+        assert np.array_equal(sl[i, :w], ref[:w]) and not sl[i, w:].any()
+
+
+@pytest.mark.parametrize("cap,sdeg", [(1, 1), (3, 128), (20, 128), (9, 63), (9, 64), (50, 700)])
+def test_poly_rem(H, oracle, cap, sdeg):
+    rng = np.random.default_rng(cap + sdeg)
+    A = _rand_polys(rng, 64, cap)
+    S = _rand_polys(rng, 1, sdeg // 64 + 1, maxdeg=sdeg)[0]
+    S[sdeg // 64] |= np.uint64(1 << (sdeg % 64))
+    ctx = make_ctx(H, (64, 64, 1, 64), 2)
+    pr = ctx.poly_rem(H.Polys.from_host(A, ctx.device), S)
+    ctx.synchronize()
+    rl, rd = pr.to_host()
+    for i in range(len(A)):
+        ref, rdeg = oracle.poly_rem(A[i], S)
+        assert rd[i] == rdeg
+        assert np.array_equal(rl[i, : len(ref)], ref) and not rl[i, len(ref):].any()
+
+
+def test_poly_rem_errors(H):
+    ctx = make_ctx(H, (64, 64, 1, 64), 3)
+    p = H.Polys.from_host(np.ones((2, 2), dtype=np.uint64), ctx.device)
+    with pytest.raises(ZeroDivisionError):
+        ctx.poly_rem(p, np.zeros(1, dtype=np.uint64))
+    with pytest.raises(H.EngineError):
+        ctx.poly_rem(p, np.ones(1, dtype=np.uint64))
+
+
+# ------------------------------------------------------------------ keys and cipher
+@pytest.mark.parametrize("params", [(64, 32, 8, 32), (128, 128, 1, 128), (256, 256, 1, 256),
+                                    (64, 64, 1, 64), (100, 27, 3, 40)])
+def test_keygen_parity(H, oracle, params):
+    ctx = make_ctx(H, params, 99)
+    sk, pk, _ = keys(*params, 99)
+    assert np.array_equal(ctx.get_secret_key().limbs, sk)
+    assert np.array_equal(ctx.get_public_key().limbs, pk)
+
+
+@pytest.mark.parametrize("params,dtype", [((64, 32, 8, 32), np.uint8), ((128, 128, 1, 128), np.uint32),
+                                          ((256, 256, 1, 256), np.uint32), ((64, 64, 1, 64), np.uint8),
+                                          ((100, 27, 3, 40), np.uint16), ((128, 128, 64, 128), np.uint64)])
+def test_encrypt_decrypt_parity(H, oracle, params, dtype):
+    d, dp, delta, tau = params
+    ctx = make_ctx(H, params, 7)
+    sk, pk, _ = keys(*params, 7)
+    n = 96
+    vals = plain(n, dtype, 8)
+    nbits = 8 * np.dtype(dtype).itemsize
+    m = masks(n, nbits, tau, 9)
+    c = ctx.encrypt(vals, masks=m)
+    dec = ctx.decrypt(c)
+    ctx.synchronize()
+    gl, gd = c.to_host()
+    bound = fresh_bound(d, dp, nbits)
+    rl, rd = oracle.encrypt_batch(pk, as_bytes(vals), m, bound)
+    assert_batches_equal(gl, gd, rl, rd, bound, n, "encrypt")
+    assert np.array_equal(dec, vals)
+    rdec = oracle.decrypt_batch(sk, rl, rd, bound, nbits, n).view(dtype).reshape(-1)
+    assert np.array_equal(rdec, dec)
+
+
+def test_decrypt_errors(H):
+    ctx = H.Context(H.Parameters(64, 32, 8, 32))
+    with pytest.raises(H.ContextCryptoError):
+        ctx.encrypt(np.array([1], dtype=np.uint8))  # public key unset
+    ctx.seed_rng(1)
+    ctx.generate_secret_key()
+    ctx.generate_public_key()
+    c = ctx.encrypt(np.array([3], dtype=np.uint8))
+    sk = ctx.get_secret_key()
+    ctx.set_secret_key(sk)
+    assert ctx.get_public_key() is None  # context.rs:656-667
+    assert ctx.decrypt(c)[0] == 3
+
+
+# ------------------------------------------------------------------ circuits
+def _pair(H, ctx, params, dtype, n, seed, lo=None, hi=None):
+    d, dp, delta, tau = params
+    nbits = 8 * np.dtype(dtype).itemsize
+    a = plain(n, dtype, seed, lo, hi)
+    b = plain(n, dtype, seed + 1, lo, hi)
+    ma, mb = masks(n, nbits, tau, seed + 2), masks(n, nbits, tau, seed + 3)
+    return a, b, ma, mb, ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb)
+
+
+@pytest.mark.parametrize("params,dtype,n", [((64, 64, 1, 64), np.uint8, 128),
+                                            ((64, 64, 1, 64), np.uint32, 32),
+                                            ((64, 16, 1, 16), np.uint8, 64),
+                                            ((128, 128, 1, 128), np.uint32, 24),
+                                            ((128, 128, 4, 128), np.uint16, 32),
+                                            ((256, 256, 1, 256), np.uint32, 4),
+                                            ((256, 128, 1, 128), np.uint64, 2)])
+def test_add_parity(H, oracle, params, dtype, n):
+    d, dp, delta, tau = params
+    ctx = make_ctx(H, params, 17)
+    sk, pk, _ = keys(*params, 17)
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, dtype, n, 18)
+    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    dec = ctx.decrypt(cs)
+    ctx.synchronize()
+    nbits = 8 * np.dtype(dtype).itemsize
+    bound = fresh_bound(d, dp, nbits)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    ob = H.add_out_bounds(bound, bound)
+    assert np.array_equal(cs.bound, ob)
+    rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, nbits, n, ob)
+    gl, gd = cs.to_host()
+    assert_batches_equal(gl, gd, rl, rd, ob, n, "add")
+    # decryption parity always; the plaintext sum only where the scheme's noise allows it
+    # ((64,64,1,64) u32 and (128,128,4,128) u16 exceed the noise budget in the reference too)
+    rdec = oracle.decrypt_batch(sk, rl, rd, ob, nbits, n).view(dtype).reshape(-1)
+    assert np.array_equal(dec, rdec)
+    if params in {(64, 16, 1, 16), (128, 128, 1, 128), (256, 256, 1, 256), (256, 128, 1, 128)}:
+        assert np.array_equal(dec, (a + b).astype(dtype))
+
+
+def test_add_edge_values(H, oracle):
+    """Wrap-around and extremes (uint.rs:202-208: 255 + 240 = 239), zero, all-ones."""
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 5)
+    sk, pk, _ = keys(*params, 5)
+    a = np.array([0, 0xFFFFFFFF, 0xFFFFFFFF, 255, 1, 0x80000000], dtype=np.uint32)
+    b = np.array([0, 1, 0xFFFFFFFF, 240, 0, 0x80000000], dtype=np.uint32)
+    n = len(a)
+    ma, mb = masks(n, 32, 128, 1), masks(n, 32, 128, 2)
+    mb[0] = 0  # an all-zero subset: encryption of 0 is the null polynomial
+    cs = ctx.apply2(H.HomomorphicAddition, ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb))
+    dec = ctx.decrypt(cs)
+    ctx.synchronize()
+    bound = fresh_bound(128, 128, 32)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    ob = H.add_out_bounds(bound, bound)
+    rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, 32, n, ob)
+    gl, gd = cs.to_host()
+    assert_batches_equal(gl, gd, rl, rd, ob, n, "add edges")
+    assert np.array_equal(dec, (a.astype(np.uint64) + b) .astype(np.uint32))
+
+
+def test_successive_add(H, oracle):
+    """uint.rs:225-252 — an add whose inputs are add outputs (non-fresh bounds)."""
+    params = (256, 128, 1, 128)
+    ctx = make_ctx(H, params, 23)
+    sk, pk, _ = keys(*params, 23)
+    n = 4
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, np.uint8, n, 24, 0, 127)
+    c = plain(n, np.uint8, 30, 0, 127)
+    mc = masks(n, 8, 128, 31)
+    cc = ctx.encrypt(c, masks=mc)
+    d1 = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    d2 = ctx.apply2(H.HomomorphicAddition, d1, cc)
+    dec = ctx.decrypt(d2)
+    ctx.synchronize()
+    assert np.array_equal(dec, (a.astype(int) + b + c).astype(np.uint8))
+    bound = fresh_bound(256, 128, 8)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    lc, dc = oracle.encrypt_batch(pk, as_bytes(c), mc, bound)
+    b1 = H.add_out_bounds(bound, bound)
+    r1l, r1d = oracle.add_batch(la, da, bound, lb, db, bound, 8, n, b1)
+    b2 = H.add_out_bounds(b1, bound)
+    r2l, r2d = oracle.add_batch(r1l, r1d, b1, lc, dc, bound, 8, n, b2)
+    gl, gd = d2.to_host()
+    assert_batches_equal(gl, gd, r2l, r2d, b2, n, "successive add")
+
+
+@pytest.mark.parametrize("params,dtype,n,signed", [((128, 64, 1, 64), np.uint8, 8, False),
+                                                   ((128, 128, 1, 128), np.uint8, 4, False),
+                                                   ((512, 64, 1, 64), np.int8, 4, True),
+                                                   ((64, 32, 1, 32), np.uint16, 2, False)])
+def test_mul_parity(H, oracle, params, dtype, n, signed):
+    d, dp, delta, tau = params
+    ctx = make_ctx(H, params, 41)
+    sk, pk, _ = keys(*params, 41)
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, dtype, n, 42)
+    cp = ctx.apply2(H.HomomorphicMultiplication, ca, cb)
+    dec = ctx.decrypt(cp)
+    ctx.synchronize()
+    nbits = 8 * np.dtype(dtype).itemsize
+    bound = fresh_bound(d, dp, nbits)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    ob = H.mul_out_bounds(bound, bound, signed)
+    rl, rd = oracle.mul_batch(la, da, bound, lb, db, bound, nbits, n, ob, signed=signed)
+    gl, gd = cp.to_host()
+    assert_batches_equal(gl, gd, rl, rd, ob, n, "mul")
+    rdec = oracle.decrypt_batch(sk, rl, rd, ob, nbits, n).view(dtype).reshape(-1)
+    assert np.array_equal(dec, rdec)
+    if params != (64, 32, 1, 32):  # the reference's own mul parameters decrypt correctly
+        assert np.array_equal(dec, (a.astype(np.int64) * b).astype(dtype))
+
+
+@pytest.mark.parametrize("op", ["and", "or", "xor", "not"])
+def test_gate_parity(H, oracle, op):
+    params = (32, 8, 8, 8) if op in ("and", "or") else (32, 16, 16, 16)
+    d, dp, delta, tau = params
+    ctx = make_ctx(H, params, 61)
+    sk, pk, _ = keys(*params, 61)
+    n = 64
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, np.uint16, n, 62)
+    opcls = {"and": H.HomomorphicAndGate, "or": H.HomomorphicOrGate,
+             "xor": H.HomomorphicXorGate, "not": H.HomomorphicNotGate}[op]
+    co = ctx.apply1(opcls, ca) if op == "not" else ctx.apply2(opcls, ca, cb)
+    dec = ctx.decrypt(co)
+    ctx.synchronize()
+    bound = fresh_bound(d, dp, 16)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    rl, rd = oracle.gate_batch(op, la, da, bound, lb, db, bound, 16, n, co.bound)
+    gl, gd = co.to_host()
+    assert_batches_equal(gl, gd, rl, rd, co.bound, n, op)
+    f = {"and": np.bitwise_and, "or": np.bitwise_or, "xor": np.bitwise_xor}
+    ref = ~a if op == "not" else f[op](a, b)
+    assert np.array_equal(dec, ref)
+
+
+def test_operation_requirements(H):
+    """Context::apply2 validation (context.rs:310-323): add needs d >= 21 delta."""
+    ctx = make_ctx(H, (64, 32, 8, 32), 3)
+    c = ctx.encrypt(np.array([1, 2], dtype=np.uint8))
+    with pytest.raises(H.OperationError) as ei:
+        ctx.apply2(H.HomomorphicAddition, c, c)
+    assert ei.value.required_min_d_over_delta == 21
+    assert ei.value.actual_d == 64 and ei.value.actual_delta == 8
+    with pytest.raises(H.OperationError):
+        ctx.apply2(H.HomomorphicMultiplication, c, c)
+    ctx.apply2(H.HomomorphicXorGate, c, c)  # d/delta = 8 >= 1
+
+
+def test_bad_input_is_flagged(H):
+    """A degree word that disagrees with the limbs is reported (device-side check)."""
+    import torch
+    ctx = make_ctx(H, (64, 64, 1, 64), 4)
+    c = ctx.encrypt(np.array([5, 6], dtype=np.uint8), masks=masks(2, 8, 64, 1))
+    ctx.synchronize()
+    d0 = int(c.degree[0, 3])
+    c.degree[0, 3] = d0 + 1 if d0 < 128 else d0 - 1  # wrong either way: top bit / stray bits
+    ctx.apply2(H.HomomorphicAddition, c, c)
+    with pytest.raises(H.EngineError):
+        ctx.synchronize()
