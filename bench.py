@@ -78,7 +78,9 @@ def make_context(world, rank, device):
     return ctx
 
 
-def time_loop(fn, steps, warmup, world):
+def time_loop(fn, steps, warmup, world, stream=None):
+    """Warmup, then time exactly `steps` calls between barrier+synchronize brackets.  HIP events
+    are recorded on the stream the kernels run on (the engine's stream)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -86,10 +88,10 @@ def time_loop(fn, steps, warmup, world):
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
+    ev0.record(stream)
     for _ in range(steps):
         fn()
-    ev1.record()
+    ev1.record(stream)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -140,11 +142,11 @@ def secondary_metrics(ctx, device, steps):
     import ctypes
 
     def encdec():
-        st = L.hm_encrypt_batch(ctx._h, data.data_ptr(), 4, m.data_ptr(), ctypes.byref(cb))
-        st |= L.hm_decrypt_batch(ctx._h, ctypes.byref(cb), dec.data_ptr())
-        assert st == 0
+        ctx._launch(lambda: L.hm_encrypt_batch(ctx._h, data.data_ptr(), 4, m.data_ptr(),
+                                               ctypes.byref(cb))
+                    | L.hm_decrypt_batch(ctx._h, ctypes.byref(cb), dec.data_ptr()), "enc+dec")
 
-    wall, _ = time_loop(encdec, steps, 2, 1)
+    wall, _ = time_loop(encdec, steps, 2, 1, ctx.stream)
     ctx.synchronize()
     ok = bool(torch.equal(dec, data))
     out["u32_encrypt_decrypt"] = {"value": n * steps / wall, "unit": "u32 enc+dec/s",
@@ -194,7 +196,8 @@ def main():
     out = H.Ciphered.empty(n, ob, device, np.dtype(np.uint32))
     ctx.synchronize()
 
-    wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, args.warmup, world)
+    wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, args.warmup, world,
+                           ctx.stream)
     ctx.synchronize()  # raises on any device-side error flag
     # verification (untimed): decrypt and compare; digests reduced over RCCL
     dec = ctx.decrypt(out)

@@ -277,7 +277,7 @@ void hm_ctx_destroy(hm_ctx *c) {
 
 hm_status hm_ctx_set_stream(hm_ctx *c, void *s) {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = (hipStream_t)s; // NULL = the device's default (null) stream, as in HIP
     return HM_OK;
 }
 

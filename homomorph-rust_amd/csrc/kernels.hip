@@ -375,8 +375,8 @@ __global__ void __launch_bounds__(256) encrypt_kernel(EncArgs E) {
             const uint32_t *pk = (const uint32_t *)(E.pk + (size_t)(i0 + ii) * PC);
 #pragma unroll
             for (int l = 0; l < PC; ++l) {
-                lo[l] = __builtin_amdgcn_bitop3_b32(lo[l], pk[2 * l], msk, 0x6a);     // lo ^ (pk & m)
-                hi[l] = __builtin_amdgcn_bitop3_b32(hi[l], pk[2 * l + 1], msk, 0x6a);
+                lo[l] ^= pk[2 * l] & msk; // one v_bitop3_b32 each (compiler-formed)
+                hi[l] ^= pk[2 * l + 1] & msk;
             }
         }
     }
@@ -435,26 +435,24 @@ int launch_encrypt(const EncArgs &E, void *stream) {
 // Decryption: bit = parity(C & z) with z_k = (X^k mod S)(0).  One wavefront per value; lanes
 // stride over the value's limbs (coalesced), accumulate per-bit parities, XOR-reduce.
 __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
-    __shared__ uint32_t offs[HM_MAX_BITS + 1];
-    if (threadIdx.x == 0) {
-        uint32_t s = 0;
-        for (uint32_t i = 0; i < D.nbits; ++i) offs[i] = s, s += cap_of(D.ib.b[i]);
-        offs[D.nbits] = s;
-    }
-    __syncthreads();
-    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const int wave = (int)rfl(threadIdx.x >> 6);
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     if (e >= D.n) return;
     const int lane = lane_id();
     const uint64_t *src = D.in.limbs + e * D.in.stride;
-    const uint32_t total = offs[D.nbits];
+    const uint32_t total = (uint32_t)D.in.stride;
     uint64_t m0 = 0, m1 = 0;
-    uint32_t i = 0;
+    // bit i of the value owns limbs [lo, hi); each lane walks its limbs in increasing order
+    uint32_t i = 0, lo = 0, hi = cap_of(D.ib.b[0]);
     bool bad = false;
     for (uint32_t g = lane; g < total; g += kWave) {
-        while (g >= offs[i + 1]) ++i;
+        while (g >= hi) {
+            ++i;
+            lo = hi;
+            hi += cap_of(D.ib.b[i]);
+        }
         const uint64_t v = src[g];
-        const uint32_t zi = g - offs[i];
+        const uint32_t zi = g - lo;
         uint64_t z = 0;
         if (zi < D.zlimbs) z = D.z[zi];
         else if (v) bad = true;
@@ -475,8 +473,10 @@ __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
 
 int launch_decrypt(const DecArgs &D, void *stream) {
     if (D.n == 0) return 0;
-    const uint64_t blocks = (D.n + 3) / 4;
-    hipLaunchKernelGGL(decrypt_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, D);
+    const char *env = getenv("HM_DEC_WPB");
+    const uint32_t wpb = env ? (uint32_t)atoi(env) : 4u;
+    const uint64_t blocks = (D.n + wpb - 1) / wpb;
+    hipLaunchKernelGGL(decrypt_kernel, dim3((unsigned)blocks), dim3(64 * wpb), 0, (hipStream_t)stream, D);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

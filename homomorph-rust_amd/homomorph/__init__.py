@@ -334,8 +334,13 @@ class Context:
                                  self.device.index or 0, ctypes.byref(h))
         _check(st, "hm_ctx_create")
         self._h = h
-        # run on torch's current stream so torch-side buffers and engine kernels are ordered
-        self.use_stream(torch.cuda.current_stream(self.device))
+        # The engine launches on a dedicated torch-created stream.  Every launching call first
+        # makes that stream wait for the caller's current stream and afterwards makes the caller's
+        # stream wait for it (event record + wait, asynchronous), so torch-side producers and
+        # consumers of the buffers are ordered with the kernels whatever stream the caller uses.
+        self._stream = torch.cuda.Stream(device=self.device)
+        _check(lib().hm_ctx_set_stream(self._h, ctypes.c_void_p(self._stream.cuda_stream)),
+               "hm_ctx_set_stream")
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -346,9 +351,18 @@ class Context:
                 pass
             self._h = None
 
-    def use_stream(self, stream):
-        _check(lib().hm_ctx_set_stream(self._h, ctypes.c_void_p(stream.cuda_stream)),
-               "hm_ctx_set_stream")
+    def _launch(self, fn, what: str):
+        torch = _torch()
+        cur = torch.cuda.current_stream(self.device)
+        self._stream.wait_stream(cur)
+        st = fn()
+        cur.wait_stream(self._stream)
+        _check(st, what)
+
+    @property
+    def stream(self):
+        """The torch stream the engine's kernels run on."""
+        return self._stream
 
     @property
     def parameters(self) -> Parameters:
@@ -430,8 +444,9 @@ class Context:
             bound = np.full(nbits, self.fresh_bound(), dtype=np.uint32)
         out = Ciphered.empty(n, bound, self.device, plain_dtype)
         c = out._c()
-        _check(lib().hm_encrypt_batch(self._h, dev_data.data_ptr(), nbytes, dev_masks.data_ptr(),
-                                      ctypes.byref(c)), "encrypt")
+        self._launch(lambda: lib().hm_encrypt_batch(self._h, dev_data.data_ptr(), nbytes,
+                                                    dev_masks.data_ptr(), ctypes.byref(c)),
+                     "encrypt")
         out._keep = (dev_data, dev_masks)
         return out
 
@@ -442,7 +457,8 @@ class Context:
             raise CipherError(_lib.ERR_INVALID_CIPHERED_LENGTH, "decrypt")
         out = torch.empty((c.n, c.nbits // 8), dtype=torch.uint8, device=self.device)
         cb = c._c()
-        _check(lib().hm_decrypt_batch(self._h, ctypes.byref(cb), out.data_ptr()), "decrypt")
+        self._launch(lambda: lib().hm_decrypt_batch(self._h, ctypes.byref(cb), out.data_ptr()),
+                     "decrypt")
         return out
 
     def decrypt(self, c: Ciphered, dtype=None) -> np.ndarray:
@@ -474,14 +490,15 @@ class Context:
                              a.plain_dtype)
         ca, cb, co = a._c(), b._c(), out._c()
         if op is HomomorphicAddition:
-            st = lib().hm_add_batch(self._h, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(co))
+            fn = lambda: lib().hm_add_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),  # noqa
+                                            ctypes.byref(co))
         elif op is HomomorphicMultiplication:
-            st = lib().hm_mul_batch(self._h, ctypes.byref(ca), ctypes.byref(cb), int(signed),
-                                    ctypes.byref(co))
+            fn = lambda: lib().hm_mul_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),  # noqa
+                                            int(signed), ctypes.byref(co))
         else:
-            st = lib().hm_gate_batch(self._h, op.CODE, ctypes.byref(ca), ctypes.byref(cb),
-                                     ctypes.byref(co))
-        _check(st, op.__name__)
+            fn = lambda: lib().hm_gate_batch(self._h, op.CODE, ctypes.byref(ca),  # noqa
+                                             ctypes.byref(cb), ctypes.byref(co))
+        self._launch(fn, op.__name__)
         return out
 
     def apply1(self, op, a: Ciphered) -> Ciphered:
@@ -490,45 +507,47 @@ class Context:
         need = gate_out_bounds(op, a.bound)
         out = Ciphered.empty(a.n, need, self.device, a.plain_dtype)
         ca, co = a._c(), out._c()
-        _check(lib().hm_gate_batch(self._h, op.CODE, ctypes.byref(ca), None, ctypes.byref(co)),
-               op.__name__)
+        self._launch(lambda: lib().hm_gate_batch(self._h, op.CODE, ctypes.byref(ca), None,
+                                                 ctypes.byref(co)), op.__name__)
         return out
 
     # ---- polynomial primitives
     def poly_add(self, a: Polys, b: Polys) -> Polys:
         out = Polys.empty(a.n, max(a.cap, b.cap), self.device)
         ca, cb, co = a._c(), b._c(), out._c()
-        _check(lib().hm_poly_add_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),
-                                       ctypes.byref(co)), "poly_add")
+        self._launch(lambda: lib().hm_poly_add_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),
+                                              ctypes.byref(co)), "poly_add")
         return out
 
     def poly_mul(self, a: Polys, b: Polys) -> Polys:
         out = Polys.empty(a.n, a.cap + b.cap, self.device)
         ca, cb, co = a._c(), b._c(), out._c()
-        _check(lib().hm_poly_mul_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),
-                                       ctypes.byref(co)), "poly_mul")
+        self._launch(lambda: lib().hm_poly_mul_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),
+                                              ctypes.byref(co)), "poly_mul")
         return out
 
     def poly_rem(self, a: Polys, s_limbs) -> Polys:
         s = np.ascontiguousarray(s_limbs, dtype=np.uint64)
         out = Polys.empty(a.n, a.cap, self.device)
         ca, co = a._c(), out._c()
-        _check(lib().hm_poly_rem_batch(self._h, ctypes.byref(ca), _p64(s), s.size,
-                                       ctypes.byref(co)), "poly_rem")
+        self._launch(lambda: lib().hm_poly_rem_batch(self._h, ctypes.byref(ca), _p64(s), s.size,
+                                                     ctypes.byref(co)), "poly_rem")
         return out
 
     def synchronize(self):
+        """Wait for the engine's stream; raise the first device-side error flagged since the
+        last check (capacity / bad input)."""
         _check(lib().hm_ctx_synchronize(self._h), "device")
 
 
 def add_into(ctx: Context, a: Ciphered, b: Ciphered, out: Ciphered) -> None:
     """hm_add_batch into a preallocated output (no allocation on the launch path)."""
     ca, cb, co = a._c(), b._c(), out._c()
-    _check(lib().hm_add_batch(ctx._h, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(co)),
-           "hm_add_batch")
+    ctx._launch(lambda: lib().hm_add_batch(ctx._h, ctypes.byref(ca), ctypes.byref(cb),
+                                           ctypes.byref(co)), "hm_add_batch")
 
 
 def mul_into(ctx: Context, a: Ciphered, b: Ciphered, out: Ciphered, signed=False) -> None:
     ca, cb, co = a._c(), b._c(), out._c()
-    _check(lib().hm_mul_batch(ctx._h, ctypes.byref(ca), ctypes.byref(cb), int(signed),
-                              ctypes.byref(co)), "hm_mul_batch")
+    ctx._launch(lambda: lib().hm_mul_batch(ctx._h, ctypes.byref(ca), ctypes.byref(cb),
+                                           int(signed), ctypes.byref(co)), "hm_mul_batch")

@@ -103,7 +103,9 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
 /* Drop: device copies of the secret key (and tables derived from it) are zeroed before release,
  * mirroring SecretKey's Drop (src/context.rs:197-206). */
 void hm_ctx_destroy(hm_ctx *ctx);
-/* Use a caller stream (hipStream_t passed as void*) instead of the context's own; NULL restores. */
+/* Launch on a caller stream (hipStream_t passed as void*; NULL = the default null stream, as in
+ * HIP) instead of the context's own non-blocking stream.  Use it to order the engine's launches
+ * with the caller's copies, e.g. torch.cuda.current_stream().cuda_stream. */
 hm_status hm_ctx_set_stream(hm_ctx *ctx, void *hip_stream);
 void *hm_ctx_stream(const hm_ctx *ctx);
 /* Parameters getters (src/context.rs:96-118). */

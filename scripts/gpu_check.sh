@@ -12,6 +12,6 @@ step() { # name limit cmd...
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
-step pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 5
+step pytest_gpu 600 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300
+step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 300 python bench.py --steps 10 --warmup 2 --cpu-seconds 5
