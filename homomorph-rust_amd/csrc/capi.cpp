@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -14,6 +15,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "gf2_wave.h"
 
 using namespace hm;
 
@@ -37,6 +39,8 @@ struct hm_ctx {
     size_t d_s_limbs = 0;
     uint32_t *d_ws = nullptr;          // multiplier workspace
     size_t ws_bytes = 0;
+    uint32_t *d_ws_add = nullptr;      // adder workspace (validated inputs, per-bit a_i*b_i)
+    size_t ws_add_bytes = 0;
     int *d_status = nullptr;
     hipError_t last_hip = hipSuccess;
 };
@@ -270,6 +274,7 @@ void hm_ctx_destroy(hm_ctx *c) {
     if (c->d_pk) (void)hipFree(c->d_pk);
     if (c->d_s) (void)hipFree(c->d_s);
     if (c->d_ws) (void)hipFree(c->d_ws);
+    if (c->d_ws_add) (void)hipFree(c->d_ws_add);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -555,41 +560,62 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     if (!covers(out, need)) return HM_ERR_INVALID_ARGUMENT;
     if (a->n == 0) return HM_OK;
 
-    // LDS plan (32-bit words per wave), simulated along the chain from the input bounds
-    uint32_t SA = 0, SB = 0;
-    for (uint32_t i = 0; i < L; ++i) {
-        SA = std::max(SA, 2 * cap_of(a->bound[i]));
-        SB = std::max(SB, 2 * cap_of(b->bound[i]));
-    }
-    const uint32_t SX = std::max(SA, SB), SAB = SA + SB, SP = SX + SAB;
-    uint32_t SC = 2;
+    // Workspace slots (words) and LDS plan per wave, from the static bounds
+    uint32_t cntA = 0, cntB = 0, cntAB = 0, cntP = 0, SC = 2, maxPw = 0;
     int64_t cb = -1;
-    for (uint32_t i = 0; i + 1 < L; ++i) {
-        const int64_t x = std::max<int64_t>(a->bound[i], b->bound[i]);
-        const int64_t ab = (int64_t)a->bound[i] + b->bound[i];
-        const int64_t p = x + ab;
-        const uint32_t need_w = std::max(words_of_bound(p) + words_of_bound(cb), words_of_bound(ab));
-        SC = std::max(SC, need_w + 2);
-        cb = (cb < 0) ? ab : std::max(ab, p + cb);
+    for (uint32_t i = 0; i < L; ++i) {
+        const int64_t ba = a->bound[i], bb = b->bound[i];
+        cntA = std::max(cntA, 2 * cap_of(a->bound[i]));
+        cntB = std::max(cntB, 2 * cap_of(b->bound[i]));
+        if (i + 1 < L) {
+            const int64_t x = std::max(ba, bb), ab = ba + bb, p = x + ab;
+            cntAB = std::max(cntAB, words_of_bound(ba) + words_of_bound(bb));
+            cntP = std::max(cntP, words_of_bound(x) + words_of_bound(ab));
+            maxPw = std::max(maxPw, words_of_bound(p));
+            SC = std::max(SC, std::max(words_of_bound(p) + words_of_bound(cb), words_of_bound(ab)) + 2);
+            cb = (cb < 0) ? ab : std::max(ab, p + cb);
+        }
     }
-    auto even = [](uint32_t v) { return (v + 3) & ~1u; };
+    cntAB = std::max(cntAB, 1u), cntP = std::max(cntP, 1u);
+    auto even = [](uint32_t v) { return (v + 1) & ~1u; };
     AddArgs A{};
+    A.cntA = cntA, A.cntB = cntB, A.cntAB = cntAB, A.cntP = cntP;
+    // the carry buffers double as the pre-phase scratch (inputs + ab_i), so size them for both
+    // A carry buffer holds a whole tile of the widest width the launch instantiates (PAD mode);
+    // each buffer sits above a zero halo of kHalo words.
+    const uint32_t need_w = (SC + 63) / 64;
+    const uint32_t wmax = need_w <= 4 ? 4 : need_w <= 8 ? 8 : need_w <= 12 ? 12 : need_w <= 16 ? 16 : 24;
+    uint32_t cw = std::max(SC, (L * (cntA + cntB + cntAB) + 1) / 2 + 1);
+    // PAD needs one tile per product (need_w <= 24) and one uniform chunk (P within kQBig
+    // words) so that window reads stay inside [-kHalo, 64*wmax)
+    A.pad = need_w <= 24 && maxPw <= 25;
+    if (A.pad) cw = std::max(cw, 64 * wmax);
+    A.cw = even(cw);
     uint32_t o = 0;
-    A.lds.oA = o, o += even(SA);
-    A.lds.oB = o, o += even(SB);
-    A.lds.oX = o, o += even(SX);
-    A.lds.oAB = o, o += even(SAB);
-    A.lds.oP = o, o += even(SP);
-    A.lds.oC0 = o, o += even(SC);
-    A.lds.oC1 = o, o += even(SC);
-    A.lds.per_wave = o;
-    A.lds.max_prod_words = std::max(SC, std::max(SP, SAB));
+    A.oP = o, o += even(L * cntP);
+    o += kHalo;
+    A.oC0 = o, o += A.cw;
+    o += kHalo;
+    A.oC1 = o, o += A.cw;
+    A.oDeg = o, o += even(2 * L);
+    A.lds_per_wave = o;
+    A.max_prod_words = SC;
+    if (const char *dbg = getenv("HM_DEBUG_SKIP")) A.debug_skip = (uint32_t)atoi(dbg);
     if ((size_t)o * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
+    A.ws_stride = ((uint64_t)L * (cntA + cntB + cntAB) + 63) & ~(uint64_t)63;
+    const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
+    DeviceGuard g(c->device);
+    if (bytes > c->ws_add_bytes) {
+        HM_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->d_ws_add) (void)hipFree(c->d_ws_add), c->d_ws_add = nullptr, c->ws_add_bytes = 0;
+        HM_HIP(c, hipMalloc(&c->d_ws_add, bytes));
+        c->ws_add_bytes = bytes;
+    }
+    A.ws = c->d_ws_add;
     A.a = batch_arg(a), A.b = batch_arg(b), A.out = batch_arg(out);
     A.n = a->n, A.nbits = L;
     A.status = c->d_status;
     fill_bounds(A.ab, a), fill_bounds(A.bb, b), fill_bounds(A.ob, out);
-    DeviceGuard g(c->device);
     return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 

@@ -19,18 +19,21 @@ struct BatchArg {
     uint64_t stride; // limbs per value
 };
 
-// Per-wave LDS carve-out of the fused adder (units: 32-bit words, all offsets even).
-struct AddLds {
-    uint32_t per_wave; // words per wave
-    uint32_t oA, oB, oX, oAB, oP, oC0, oC1;
-    uint32_t max_prod_words; // largest product output (words) along the chain
-};
-
+// Fused adder.  Per value, a global workspace (ws_stride words) holds the validated inputs and
+// the per-bit products ab_i; each wave's LDS holds the per-bit P_i and the carry double buffer.
 struct AddArgs {
     BatchArg a, b, out;
     uint64_t n;
     uint32_t nbits;
-    AddLds lds;
+    uint32_t *ws;        // [A slots: nbits*cntA][B slots: nbits*cntB][AB slots: nbits*cntAB]
+    uint64_t ws_stride;  // words per value
+    uint32_t cntA, cntB, cntAB, cntP; // slot sizes in words (cntAB = cntA+cntB, cntP = max(cntA,cntB)+cntAB)
+    uint32_t lds_per_wave;            // words
+    uint32_t oP, oC0, oC1, oDeg;      // LDS offsets (words): P slots, carry buffers, degree table
+    uint32_t cw;                      // carry buffer words
+    uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
+    uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)
+    uint32_t debug_skip;              // timing experiments only (HM_DEBUG_SKIP): 1 pre-phase, 2 chain product
     int *status;
     Bounds ab, bb, ob;
 };

@@ -22,6 +22,7 @@
 namespace hm {
 
 constexpr int kWave = 64;
+constexpr int kHalo = 32; // zero words below a padded V buffer (>= the uniform chunk QC)
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -44,6 +45,12 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t old) {
 
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+// acc ^ (x & m) in one v_bitop3_b32 (truth table index = S0*4 + S1*2 + S2 with S0 = x,
+// S1 = acc, S2 = m  ->  0x6c; the compiler does not always fuse the and/xor pair itself).
+__device__ __forceinline__ uint32_t xor_and(uint32_t acc, uint32_t x, uint32_t m) {
+    return __builtin_amdgcn_bitop3_b32(x, acc, m, 0x6c);
 }
 
 __device__ __forceinline__ int wave_max_i32(int v) {
@@ -80,7 +87,7 @@ __device__ __forceinline__ int wave_top_ordered(int ldeg) {
 //  tile covers output words [base, base + 64*W) ∩ [0, nout)
 // MULTI: the tile does not start at word 0, so lane 0 tracks word base-1 to shift its top bit in.
 // Returns the tile's highest set bit index (global), or -1.
-template <int W, int QC, bool MULTI>
+template <int W, int QC, bool MULTI, bool MASKED, bool PAD>
 __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
                                         const uint32_t *__restrict__ V, int nv,
                                         const uint32_t *__restrict__ Add, int nadd,
@@ -104,11 +111,22 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
 #pragma unroll
         for (int k = 0; k < W + QC; ++k) {
             const int idx = cb + k;
-            cx[k] = (idx >= 0 && idx < nv) ? V[idx] : 0u;
+            if constexpr (PAD) cx[k] = V[idx]; // zero halo below, zeros above nv
+            else cx[k] = (idx >= 0 && idx < nv) ? V[idx] : 0u;
         }
-        uint32_t u[QC];
+        // Decision bits.  Branchy form: transposed, lane r holds col_r = sum_q bit r of U[q0+q]
+        // << q, so each (q, r) decision is one scalar bit test of a readlane'd column
+        // (s_bitcmp + s_cbranch) guarding W XORs.  Masked form (small W, where the scalar unit
+        // shared by the CU's waves would be the bottleneck): the U words stay in VGPRs and every
+        // (q, r) costs one v_bfe_i32 mask plus W v_bitop3 (t ^ (cx & mask)), no branches.
+        uint32_t colv = 0u;
+        uint32_t uv[MASKED ? QC : 1];
 #pragma unroll
-        for (int q = 0; q < QC; ++q) u[q] = (q0 + q < nu) ? rfl(U[q0 + q]) : 0u;
+        for (int q = 0; q < QC; ++q) {
+            const uint32_t uq = (q0 + q < nu) ? U[q0 + q] : 0u; // uniform address: broadcast read
+            if constexpr (MASKED) uv[q] = uq;
+            else colv |= ((uq >> (lane & 31)) & 1u) << q;
+        }
 
         uint32_t t[W];
 #pragma unroll
@@ -121,13 +139,24 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
             for (int j = W - 1; j >= 1; --j) t[j] = funnel(t[j], t[j - 1], 31);
             t[0] = funnel(t[0], prev, 31);
             if (MULTI) tlo <<= 1;
+            if constexpr (MASKED) {
 #pragma unroll
-            for (int q = 0; q < QC; ++q) {
-                if ((u[q] >> r) & 1u) {
-                    asm volatile("" ::);
+                for (int q = 0; q < QC; ++q) {
+                    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)uv[q], r, 1);
 #pragma unroll
-                    for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC];
-                    if (MULTI) tlo ^= cx[QC - 1 - q];
+                    for (int j = 0; j < W; ++j) t[j] = xor_and(t[j], cx[j - q + QC], m);
+                    if (MULTI) tlo = xor_and(tlo, cx[QC - 1 - q], m);
+                }
+            } else {
+                const uint32_t col = (uint32_t)__builtin_amdgcn_readlane((int)colv, r);
+#pragma unroll
+                for (int q = 0; q < QC; ++q) {
+                    if (__builtin_expect((col & (1u << q)) != 0, 1)) {
+                        asm volatile("" ::);
+#pragma unroll
+                        for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC];
+                        if (MULTI) tlo ^= cx[QC - 1 - q];
+                    }
                 }
             }
         }
@@ -137,7 +166,7 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
     int ldeg = -1;
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-        if (w0 + j < nout) {
+        if (PAD || w0 + j < nout) { // PAD: the whole tile is written (zeros past nout)
             Dst[w0 + j] = acc[j];
             if (acc[j]) ldeg = (w0 + j) * 32 + 31 - __builtin_clz(acc[j]);
         }
@@ -145,13 +174,17 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
     return wave_top_ordered(ldeg);
 }
 
-template <int QC, int W, int WMAX>
+// Tile widths up to this use the masked (branch-free) decision form.
+constexpr int kMaskedMaxW = 0; // measured: the masked form lost at every width tried
+
+template <int QC, int W, int WMAX, bool PAD>
 __device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32_t *V, int nv,
                                          const uint32_t *Add, int nadd, uint32_t *Dst, int nout) {
-    int top = mul_tile<W, QC, false>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
-    if constexpr (W == WMAX) { // only the widest tile ever needs more than one pass
+    constexpr bool kMasked = W <= kMaskedMaxW;
+    int top = mul_tile<W, QC, false, kMasked, PAD>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
+    if constexpr (W == WMAX && !PAD) { // only the widest tile ever needs more than one pass
         for (int base = kWave * W; base < nout; base += kWave * W) {
-            int t = mul_tile<W, QC, true>(U, nu, V, nv, Add, nadd, Dst, nout, base);
+            int t = mul_tile<W, QC, true, kMasked, false>(U, nu, V, nv, Add, nadd, Dst, nout, base);
             if (t >= 0) top = t;
         }
     }
@@ -162,7 +195,9 @@ __device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32
 // Dst must not alias U, V or Add.  The per-lane tile width W is picked from nout among the
 // instantiated widths <= WMAX (the kernel's VGPR budget is set by WMAX + QC); longer outputs are
 // produced in several WMAX-wide tiles.
-template <int QC, int WMAX>
+// PAD (caller guarantees): V has >= kHalo zero words below it and zeros from nv up to 64*WMAX,
+// Dst has room for 64*W words, and nout <= 64*WMAX (one tile).
+template <int QC, int WMAX, bool PAD = false>
 __device__ __forceinline__ int wave_mul(const uint32_t *U, int nu, const uint32_t *V, int nv,
                                         const uint32_t *Add, int nadd, uint32_t *Dst,
                                         int *nout_p) {
@@ -172,19 +207,23 @@ __device__ __forceinline__ int wave_mul(const uint32_t *U, int nu, const uint32_
     const int w = (nout + kWave - 1) / kWave;
 #define HM_TRY_W(WW)                                                                              \
     if constexpr (WW < WMAX) {                                                                    \
-        if (w <= WW) return mul_tiles<QC, WW, WMAX>(U, nu, V, nv, Add, nadd, Dst, nout);          \
+        if (w <= WW) return mul_tiles<QC, WW, WMAX, PAD>(U, nu, V, nv, Add, nadd, Dst, nout);          \
     }
     HM_TRY_W(1)
     HM_TRY_W(2)
     HM_TRY_W(3)
     HM_TRY_W(4)
+    HM_TRY_W(5)
     HM_TRY_W(6)
+    HM_TRY_W(7)
     HM_TRY_W(8)
+    HM_TRY_W(9)
     HM_TRY_W(10)
+    HM_TRY_W(11)
     HM_TRY_W(12)
     HM_TRY_W(16)
 #undef HM_TRY_W
-    return mul_tiles<QC, WMAX, WMAX>(U, nu, V, nv, Add, nadd, Dst, nout);
+    return mul_tiles<QC, WMAX, WMAX, PAD>(U, nu, V, nv, Add, nadd, Dst, nout);
 }
 
 // Dst[0..n) = A ^ B (n = max(na, nb)); exact degree (-1 = null).  Strided lane loop.

@@ -21,12 +21,19 @@ __device__ __forceinline__ void flag(int *status, int code) {
     if (status) atomicCAS(status, 0, code);
 }
 
-// Make this wave's LDS / global writes visible to its own later reads by other lanes, and keep
-// the compiler from reordering memory operations across the point.
+// wsync: order this wave's LDS writes before its later LDS reads by other lanes.  A wave's LDS
+// instructions execute in order, so only the compiler must be kept from reordering (wavefront
+// scope emits no wait).  gsync: the same for GLOBAL memory, where a lane's load must not overtake
+// another lane's earlier store: workgroup scope drains vmcnt/lgkmcnt.
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void gsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 __device__ __forceinline__ uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
@@ -95,81 +102,226 @@ __device__ int store_xor_bit(const uint32_t *X, int nx, const uint32_t *C, int n
 
 __device__ __forceinline__ int words_of(int deg) { return deg >= 0 ? nwords(deg) : 0; }
 
+// dst (cap limbs) = A ^ B ^ C (output bit of the adder); writes the exact degree.
+__device__ int store_xor3_bit(const uint32_t *Aw, int na, const uint32_t *Bw, int nb,
+                              const uint32_t *C, int nc, uint64_t *__restrict__ dst,
+                              uint32_t bound, uint32_t *deg_out, int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int n = max(max(na, nb), nc);
+    const int total = max(cap, (n + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        uint32_t lo = (w < na ? Aw[w] : 0u) ^ (w < nb ? Bw[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        uint32_t hi = (w + 1 < na ? Aw[w + 1] : 0u) ^ (w + 1 < nb ? Bw[w + 1] : 0u) ^
+                      (w + 1 < nc ? C[w + 1] : 0u);
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
 // Small products (fresh operands: 9 words at d+dp = 256) use a short uniform chunk; the carry
 // product P * carry uses a chunk that covers P (25 words at d+dp = 256) in one pass.
 constexpr int kQSmall = 10;
 constexpr int kQBig = 25;
 
 // ---------------------------------------------------------------------------------------------
-// Fused ripple-carry adder.  Per bit i (common.rs:43-53):
+// Low word of (u * (v1:v0)) >> 0 restricted to the window: XOR over set bits r of u of the
+// funnel-shifted pair (v1 << r | v0 >> (32 - r)).  Four independent accumulators break the
+// dependent bitop3 chain (VALU latency) into four interleaved chains.
+__device__ __forceinline__ uint32_t clmul_word_step(uint32_t u, uint32_t v1, uint32_t v0) {
+    uint32_t a0 = v1 & (0u - (u & 1u)), a1 = 0u, a2 = 0u, a3 = 0u;
+#pragma unroll
+    for (int r = 1; r < 32; r += 4) {
+        a1 = xor_and(a1, funnel(v1, v0, 32 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r, 1));
+        a2 = xor_and(a2, funnel(v1, v0, 31 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r + 1, 1));
+        a3 = xor_and(a3, funnel(v1, v0, 30 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r + 2, 1));
+        if (r + 3 < 32)
+            a0 = xor_and(a0, funnel(v1, v0, 29 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r + 3, 1));
+    }
+    return a0 ^ a1 ^ a2 ^ a3;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-lane carry-less product word: word m of U*V (U: nu words, V: nv words).  Branch-free:
+// every bit r of U_q selects (by a sign-extended mask) the funnel-shifted V window.  Used where
+// lanes work on DIFFERENT products (no uniform operand), i.e. the adder's pre-phase.
+__device__ __forceinline__ uint32_t clmul_word(const uint32_t *__restrict__ pu, int nu,
+                                               const uint32_t *__restrict__ pv, int nv, int m) {
+    uint32_t acc = 0u;
+    const int qlo = max(0, m - nv), qhi = min(nu - 1, m);
+    for (int q = qlo; q <= qhi; ++q) {
+        const uint32_t u = pu[q];
+        const int k = m - q;
+        const uint32_t v1 = k < nv ? pv[k] : 0u;
+        const uint32_t v0 = (k >= 1 && k - 1 < nv) ? pv[k - 1] : 0u;
+        acc ^= clmul_word_step(u, v1, v0);
+    }
+    return acc;
+}
+
+__device__ __forceinline__ int bitwords(int degp1) { return degp1 ? ((degp1 - 1) >> 5) + 1 : 0; }
+
+// ---------------------------------------------------------------------------------------------
+// Fused ripple-carry adder, one wavefront per value.  Per bit i (common.rs:43-53):
 //   x = a_i ^ b_i;  s_i = x ^ carry;
 //   carry' = (x & carry) ^ (a_i & b_i) & ((x & carry) ^ 1)
-//          = ab ^ P * carry  with  ab = a_i b_i,  P = x (1 ^ ab)            (GF(2)[X] ring identity)
-// so each bit costs two small products (ab, x*ab) and ONE large product P * carry instead of the
-// reference's three large ones.  The carry stays in LDS for the whole chain.
-template <int WMAX>
+//          = ab_i ^ P_i * carry,   ab_i = a_i b_i,   P_i = x (1 ^ ab_i)   (GF(2)[X] ring identity)
+// ab_i and P_i do not depend on the carry, so they are all computed up front by a SIMT pre-phase
+// in which lanes work on different bits (branch-free per-lane products).  The sequential chain
+// then costs ONE product per bit, P_i * carry, with P_i wave-uniform (scalar branches over its
+// bits, Horner over bit positions) and the carry resident in LDS for the whole chain.
+template <int WMAX, bool PAD>
 __global__ void __launch_bounds__(256) add_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
     const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     if (e >= A.n) return; // whole wave exits together
     const int lane = lane_id();
-    uint32_t *L = lds + (size_t)wave * A.lds.per_wave;
-    uint32_t *Ab = L + A.lds.oA, *Bb = L + A.lds.oB, *X = L + A.lds.oX, *AB = L + A.lds.oAB;
-    uint32_t *P = L + A.lds.oP, *C = L + A.lds.oC0, *Cn = L + A.lds.oC1;
+    const uint32_t L = A.nbits;
+    uint32_t *Ls = lds + (size_t)wave * A.lds_per_wave;
+    uint32_t *Pall = Ls + A.oP, *C = Ls + A.oC0, *Cn = Ls + A.oC1;
+    uint32_t *degAB = Ls + A.oDeg, *degP = degAB + L; // stored as degree+1, 0 = null
+    uint32_t *ws = A.ws + e * A.ws_stride;
+    uint32_t *Aall = ws, *Ball = ws + (size_t)L * A.cntA, *ABall = Ball + (size_t)L * A.cntB;
     const uint64_t *pa = A.a.limbs + e * A.a.stride;
     const uint64_t *pb = A.b.limbs + e * A.b.stride;
     uint64_t *po = A.out.limbs + e * A.out.stride;
-    const uint32_t *da = A.a.degree + e * A.nbits;
-    const uint32_t *db = A.b.degree + e * A.nbits;
-    uint32_t *dout = A.out.degree + e * A.nbits;
+    const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
+    uint32_t *dout = A.out.degree + e * L;
 
+    // ---- phase 0: validated, masked inputs into the workspace (word slots per bit), plus an LDS
+    // copy for the pre-phase.  The pre-phase scratch (inputs, ab_i) overlays the carry buffers,
+    // which are not live until the chain starts.
+    uint32_t *Al = C, *Bl = C + (size_t)L * A.cntA, *ABl = Bl + (size_t)L * A.cntB;
+    for (uint32_t i = 0, offa = 0, offb = 0; i < L; ++i) {
+        load_bit(pa + offa, rfl(da[i]), A.ab.b[i], Aall + (size_t)i * A.cntA, A.status);
+        load_bit(pb + offb, rfl(db[i]), A.bb.b[i], Ball + (size_t)i * A.cntB, A.status);
+        offa += cap_of(A.ab.b[i]);
+        offb += cap_of(A.bb.b[i]);
+    }
+    for (uint32_t k = lane; k < 2 * L; k += kWave) degAB[k] = 0u;
+    gsync();
+    for (uint32_t k = lane; k < L * A.cntA; k += kWave) Al[k] = Aall[k];
+    for (uint32_t k = lane; k < L * A.cntB; k += kWave) Bl[k] = Ball[k];
+    wsync();
+
+    // word count of input bit i (0 = null polynomial); per lane
+    auto in_words = [&](const uint32_t *deg, const uint32_t *slot0, uint32_t cnt, uint32_t i) {
+        const uint32_t d = deg[i];
+        if (d == 0) return (slot0[(size_t)i * cnt] & 1u) ? 1 : 0;
+        return (int)(d >> 5) + 1;
+    };
+
+    // ---- phase 1: ab_i = a_i * b_i for every bit but the last (lanes over (bit, word))
+    const uint32_t nprod = (A.debug_skip & 1u) ? 0u : L - 1;
+    for (uint32_t f0 = 0; f0 < nprod * A.cntAB; f0 += kWave) {
+        const uint32_t f = f0 + lane;
+        if (f < nprod * A.cntAB) {
+            const uint32_t i = f / A.cntAB, m = f % A.cntAB;
+            const int na = in_words(da, Al, A.cntA, i), nb = in_words(db, Bl, A.cntB, i);
+            uint32_t w = 0u;
+            if ((int)m < na + nb) {
+                const uint32_t *ai = Al + (size_t)i * A.cntA, *bi = Bl + (size_t)i * A.cntB;
+                w = na <= nb ? clmul_word(ai, na, bi, nb, (int)m) : clmul_word(bi, nb, ai, na, (int)m);
+            }
+            ABl[(size_t)i * A.cntAB + m] = w;
+            ABall[(size_t)i * A.cntAB + m] = w;
+            if (w) atomicMax(&degAB[i], m * 32 + 32 - __builtin_clz(w));
+        }
+    }
+    gsync(); // ab_i in the workspace is read by other lanes in the chain
+
+    // ---- phase 2: P_i = x_i ^ x_i * ab_i,  x_i = a_i ^ b_i   (into LDS)
+    for (uint32_t f0 = 0; f0 < nprod * A.cntP; f0 += kWave) {
+        const uint32_t f = f0 + lane;
+        if (f < nprod * A.cntP) {
+            const uint32_t i = f / A.cntP, m = f % A.cntP;
+            const uint32_t *ai = Al + (size_t)i * A.cntA, *bi = Bl + (size_t)i * A.cntB;
+            const int na = in_words(da, Al, A.cntA, i), nb = in_words(db, Bl, A.cntB, i);
+            const int nx = max(na, nb);
+            const int nab = bitwords((int)degAB[i]);
+            const uint32_t *abi = ABl + (size_t)i * A.cntAB;
+            uint32_t w = 0u;
+            if ((int)m < nx + nab) {
+                // U = x_i (formed on the fly), V = ab_i
+                uint32_t acc = 0u;
+                const int qlo = max(0, (int)m - nab), qhi = min(nx - 1, (int)m);
+                for (int q = qlo; q <= qhi; ++q) {
+                    const uint32_t u = (q < na ? ai[q] : 0u) ^ (q < nb ? bi[q] : 0u);
+                    const int k = (int)m - q;
+                    const uint32_t v1 = k < nab ? abi[k] : 0u;
+                    const uint32_t v0 = (k >= 1 && k - 1 < nab) ? abi[k - 1] : 0u;
+                    acc ^= clmul_word_step(u, v1, v0);
+                }
+                w = acc;
+                if ((int)m < nx) w ^= ((int)m < na ? ai[m] : 0u) ^ ((int)m < nb ? bi[m] : 0u);
+            }
+            Pall[(size_t)i * A.cntP + m] = w;
+            if (w) atomicMax(&degP[i], m * 32 + 32 - __builtin_clz(w));
+        }
+    }
+    wsync();
+
+    // ---- phase 3: the carry chain.  The carry buffers (which held the pre-phase scratch) are
+    // zeroed with their halos, so the product's window reads need no bounds checks (PAD).
+    for (uint32_t k = lane; k < 2 * (A.cw + kHalo); k += kWave) Ls[A.oC0 - kHalo + k] = 0u;
+    wsync();
     int nc = 0; // carry words (0 = null carry, common.rs:39)
-    uint32_t offa = 0, offb = 0, offo = 0;
-    for (uint32_t i = 0; i < A.nbits; ++i) {
+    uint32_t offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t *ai = Aall + (size_t)i * A.cntA, *bi = Ball + (size_t)i * A.cntB;
         const uint32_t dga = rfl(da[i]), dgb = rfl(db[i]);
-        const int na = load_bit(pa + offa, dga, A.ab.b[i], Ab, A.status);
-        const int nb = load_bit(pb + offb, dgb, A.bb.b[i], Bb, A.status);
-        wsync();
-        const int nx = words_of(wave_xor(Ab, na, Bb, nb, X));
-        wsync();
-        store_xor_bit(X, nx, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
-        if (i + 1 < A.nbits) {
+        const int na = dga ? (int)(dga >> 5) + 1 : (int)(rfl(ai[0]) & 1u);
+        const int nb = dgb ? (int)(dgb >> 5) + 1 : (int)(rfl(bi[0]) & 1u);
+        store_xor3_bit(ai, na, bi, nb, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
+        if (i + 1 < L && !(A.debug_skip & 2u)) {
+            const int np = bitwords((int)rfl(degP[i])), nab = bitwords((int)rfl(degAB[i]));
             int nout;
-            const int nab = words_of(wave_mul<kQSmall, WMAX>(Ab, na, Bb, nb, nullptr, 0, AB, &nout));
-            wsync();
-            const int np = words_of(wave_mul<kQSmall, WMAX>(X, nx, AB, nab, X, nx, P, &nout));
-            wsync();
-            nc = words_of(wave_mul<kQBig, WMAX>(P, np, C, nc, AB, nab, Cn, &nout));
+            nc = words_of(wave_mul<kQBig, WMAX, PAD>(Pall + (size_t)i * A.cntP, np, C, nc,
+                                                     ABall + (size_t)i * A.cntAB, nab, Cn, &nout));
             wsync();
             uint32_t *t = C;
             C = Cn;
             Cn = t;
         }
-        offa += cap_of(A.ab.b[i]);
-        offb += cap_of(A.bb.b[i]);
         offo += cap_of(A.ob.b[i]);
     }
-    (void)lane;
 }
 
 int launch_add(const AddArgs &a, void *stream) {
     const int wpb = kAddWavesPerBlock;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     if (blocks == 0) return 0;
-    const size_t lds = (size_t)a.lds.per_wave * 4 * wpb;
+    const size_t lds = (size_t)a.lds_per_wave * 4 * wpb;
     // the widest per-lane tile the carry chain needs (carry + P words over 64 lanes)
-    const uint32_t need = (a.lds.max_prod_words + 63) / 64;
-    if (need <= 4)
-        hipLaunchKernelGGL(add_kernel<4>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
-    else if (need <= 8)
-        hipLaunchKernelGGL(add_kernel<8>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
-    else if (need <= 12)
-        hipLaunchKernelGGL(add_kernel<12>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
-    else if (need <= 16)
-        hipLaunchKernelGGL(add_kernel<16>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL(add_kernel<24>, dim3((unsigned)blocks), dim3(64 * wpb), lds, (hipStream_t)stream, a);
+    const uint32_t need = (a.max_prod_words + 63) / 64;
+    // PAD: every carry product fits one tile of the kernel's widest width, so the zero-padded
+    // carry buffers are read without bounds checks and written whole.
+    const bool pad = a.pad != 0;
+#define HM_LAUNCH_ADD(WM)                                                                         \
+    do {                                                                                          \
+        if (pad)                                                                                  \
+            hipLaunchKernelGGL((add_kernel<WM, true>), dim3((unsigned)blocks), dim3(64 * wpb), lds, \
+                               (hipStream_t)stream, a);                                           \
+        else                                                                                      \
+            hipLaunchKernelGGL((add_kernel<WM, false>), dim3((unsigned)blocks), dim3(64 * wpb),   \
+                               lds, (hipStream_t)stream, a);                                      \
+    } while (0)
+    if (need <= 4) HM_LAUNCH_ADD(4);
+    else if (need <= 8) HM_LAUNCH_ADD(8);
+    else if (need <= 12) HM_LAUNCH_ADD(12);
+    else if (need <= 16) HM_LAUNCH_ADD(16);
+    else HM_LAUNCH_ADD(24);
+#undef HM_LAUNCH_ADD
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -276,7 +428,7 @@ __global__ void __launch_bounds__(256) mul_kernel(MulArgs M) {
             ob += cap_of(M.bb.b[i]);
         }
     }
-    wsync();
+    gsync();
     uint32_t *Tmp = ws + M.oTmp;
     uint32_t offo = 0;
     for (uint32_t i = 0; i < L; ++i) {
@@ -299,7 +451,7 @@ __global__ void __launch_bounds__(256) mul_kernel(MulArgs M) {
             const int np = words_of(wave_mul<kQBig, 8>(Ain + 2 * oa, xa, Bin + 2 * ob, xb,
                                                     (flips & 1) ? one : nullptr, flips & 1, Tmp,
                                                     &nout));
-            wsync();
+            gsync();
             if (push) {
                 // carries.push(pp & result[i])  (common.rs:83-87): the smaller operand is uniform
                 int c;
@@ -308,10 +460,10 @@ __global__ void __launch_bounds__(256) mul_kernel(MulArgs M) {
                 if ((uint32_t)nout > sc) flag(M.status, HM_ERR_CAPACITY);
                 if (lane == 0) cwc[k] = words_of(c);
                 ++k;
-                wsync();
+                gsync();
             }
             nr = words_of(ws_xor_into(R, nr, Tmp, np));
-            wsync();
+            gsync();
         }
         const int cur_len = (int)(i * (i + 1) / 2);
         for (int j = 0; j < cur_len; ++j) {
@@ -324,15 +476,15 @@ __global__ void __launch_bounds__(256) mul_kernel(MulArgs M) {
                 if ((uint32_t)nout > sc) flag(M.status, HM_ERR_CAPACITY);
                 if (lane == 0) cwc[k] = words_of(c);
                 ++k;
-                wsync();
+                gsync();
             }
             nr = words_of(ws_xor_into(R, nr, Cj, ncj));
-            wsync();
+            gsync();
         }
         store_xor_bit(R, nr, nullptr, 0, M.out.limbs + e * M.out.stride + offo, M.ob.b[i],
                       M.out.degree + e * L + i, M.status);
         offo += cap_of(M.ob.b[i]);
-        wsync();
+        gsync();
     }
 }
 
