@@ -560,7 +560,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     if (!covers(out, need)) return HM_ERR_INVALID_ARGUMENT;
     if (a->n == 0) return HM_OK;
 
-    // Workspace slots (words) and LDS plan per wave, from the static bounds
+    // Workspace slots (words) and LDS plans, from the static bounds
     uint32_t cntA = 0, cntB = 0, cntAB = 0, cntP = 0, SC = 2, maxPw = 0;
     int64_t cb = -1;
     for (uint32_t i = 0; i < L; ++i) {
@@ -580,29 +580,29 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     auto even = [](uint32_t v) { return (v + 1) & ~1u; };
     AddArgs A{};
     A.cntA = cntA, A.cntB = cntB, A.cntAB = cntAB, A.cntP = cntP;
-    // the carry buffers double as the pre-phase scratch (inputs + ab_i), so size them for both
-    // A carry buffer holds a whole tile of the widest width the launch instantiates (PAD mode);
-    // each buffer sits above a zero halo of kHalo words.
+    // prep: enough waves per value to keep the chip busy (bits are dealt round-robin)
+    {
+        const uint64_t want = (16384 + a->n - 1) / a->n;
+        A.wpv = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 8, (uint64_t)L}));
+        const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
+        A.prep_lds = even(bpw * (cntA + cntB + cntAB) + 2 * bpw);
+        if ((size_t)A.prep_lds * 4 * 4 > 160 * 1024) return HM_ERR_UNSUPPORTED;
+    }
+    // chain: a carry buffer holds a whole tile of the widest width instantiated (PAD mode);
+    // each buffer sits above a zero halo of kHalo words
     const uint32_t need_w = (SC + 63) / 64;
     const uint32_t wmax = need_w <= 4 ? 4 : need_w <= 8 ? 8 : need_w <= 12 ? 12 : need_w <= 16 ? 16 : 24;
-    uint32_t cw = std::max(SC, (L * (cntA + cntB + cntAB) + 1) / 2 + 1);
     // PAD needs one tile per product (need_w <= 24) and one uniform chunk (P within kQBig
     // words) so that window reads stay inside [-kHalo, 64*wmax)
     A.pad = need_w <= 24 && maxPw <= 25;
+    uint32_t cw = SC;
     if (A.pad) cw = std::max(cw, 64 * wmax);
     A.cw = even(cw);
-    uint32_t o = 0;
-    A.oP = o, o += even(L * cntP);
-    o += kHalo;
-    A.oC0 = o, o += A.cw;
-    o += kHalo;
-    A.oC1 = o, o += A.cw;
-    A.oDeg = o, o += even(2 * L);
-    A.lds_per_wave = o;
+    A.chain_lds = even(2 * (A.cw + kHalo) + (L - 1) * cntP);
     A.max_prod_words = SC;
+    if ((size_t)A.chain_lds * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
     if (const char *dbg = getenv("HM_DEBUG_SKIP")) A.debug_skip = (uint32_t)atoi(dbg);
-    if ((size_t)o * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
-    A.ws_stride = ((uint64_t)L * (cntA + cntB + cntAB) + 63) & ~(uint64_t)63;
+    A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2) + 63) & ~(uint64_t)63;
     const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
     DeviceGuard g(c->device);
     if (bytes > c->ws_add_bytes) {

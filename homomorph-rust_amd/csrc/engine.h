@@ -19,21 +19,25 @@ struct BatchArg {
     uint64_t stride; // limbs per value
 };
 
-// Fused adder.  Per value, a global workspace (ws_stride words) holds the validated inputs and
-// the per-bit products ab_i; each wave's LDS holds the per-bit P_i and the carry double buffer.
+// Fused adder, two launches.  add_prep_kernel (several waves per value, lanes over (bit, word))
+// validates the inputs and computes every per-bit product ab_i = a_i b_i and P_i = x_i (1 ^ ab_i)
+// into a global workspace; add_chain_kernel (one wave per value) runs the sequential carry chain.
+// Workspace per value (ws_stride words): [ab slots: nbits*cntAB][P slots: nbits*cntP]
+// [deg(ab)+1: nbits][deg(P)+1: nbits].
 struct AddArgs {
     BatchArg a, b, out;
     uint64_t n;
     uint32_t nbits;
-    uint32_t *ws;        // [A slots: nbits*cntA][B slots: nbits*cntB][AB slots: nbits*cntAB]
-    uint64_t ws_stride;  // words per value
-    uint32_t cntA, cntB, cntAB, cntP; // slot sizes in words (cntAB = cntA+cntB, cntP = max(cntA,cntB)+cntAB)
-    uint32_t lds_per_wave;            // words
-    uint32_t oP, oC0, oC1, oDeg;      // LDS offsets (words): P slots, carry buffers, degree table
-    uint32_t cw;                      // carry buffer words
+    uint32_t *ws;
+    uint64_t ws_stride;               // words per value
+    uint32_t cntA, cntB, cntAB, cntP; // slot sizes in words (cntA = 2*max cap of a, ...)
+    uint32_t wpv;                     // prep: waves per value (bits are dealt round-robin)
+    uint32_t prep_lds;                // prep: LDS words per wave
+    uint32_t chain_lds;               // chain: LDS words per wave (two zero-haloed carry buffers)
+    uint32_t cw;                      // chain: carry buffer words
     uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
     uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)
-    uint32_t debug_skip;              // timing experiments only (HM_DEBUG_SKIP): 1 pre-phase, 2 chain product
+    uint32_t debug_skip;              // timing experiments only (HM_DEBUG_SKIP): 1 prep, 2 chain product
     int *status;
     Bounds ab, bb, ob;
 };

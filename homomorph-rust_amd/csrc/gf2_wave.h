@@ -82,12 +82,16 @@ __device__ __forceinline__ int wave_top_ordered(int ldeg) {
 
 // One output tile of  Dst = Add ^ U*V.
 //  U  : nu uniform-operand words (any address space; read with wave-uniform addresses)
-//  V  : nv words, read per lane with bounds checks (no halo needed)
+//  V  : nv words, read per lane (bounds-checked unless PAD)
 //  Add: nadd words XORed into the result (may be nullptr with nadd = 0)
 //  tile covers output words [base, base + 64*W) ∩ [0, nout)
 // MULTI: the tile does not start at word 0, so lane 0 tracks word base-1 to shift its top bit in.
+// PAIR: two bit positions per Horner step (t = X^2 t + X S_{r+1} + S_r) with a pre-shifted copy
+//   of the V window (cx1 = X*window).  When both bits of a (q, pair) are set the two windows are
+//   folded with one v_bitop3 xor3, so the XOR work per pair drops from 1.0 W to 0.75 W on average,
+//   and the half-rate v_alignbit shifts run once per pair instead of once per bit.
 // Returns the tile's highest set bit index (global), or -1.
-template <int W, int QC, bool MULTI, bool MASKED, bool PAD>
+template <int W, int QC, bool MULTI, bool PAIR, bool PAD>
 __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
                                         const uint32_t *__restrict__ V, int nv,
                                         const uint32_t *__restrict__ Add, int nadd,
@@ -105,57 +109,86 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
     for (int q0 = 0; q0 < nu; q0 += QC) {
         // U chunk words [q0, q0+QC) reach output words [q0, q0 + QC + nv)
         if (q0 >= tile_end || base >= q0 + QC + nv) continue;
-        // window: cx[k] = V[w0 - q0 - QC + k], k in [0, W+QC)
-        uint32_t cx[W + QC];
-        const int cb = w0 - q0 - QC;
+        // window: cx[k] = V[w0 - q0 - QC - 1 + k], k in [0, W+QC+1); the word for (j, q) is
+        // cx[j - q + QC + 1]; word base-1 (MULTI) uses cx[QC - q]
+        constexpr int NX = W + QC + 1;
+        uint32_t cx[NX];
+        const int cb = w0 - q0 - QC - 1;
 #pragma unroll
-        for (int k = 0; k < W + QC; ++k) {
+        for (int k = 0; k < NX; ++k) {
             const int idx = cb + k;
             if constexpr (PAD) cx[k] = V[idx]; // zero halo below, zeros above nv
             else cx[k] = (idx >= 0 && idx < nv) ? V[idx] : 0u;
         }
-        // Decision bits.  Branchy form: transposed, lane r holds col_r = sum_q bit r of U[q0+q]
-        // << q, so each (q, r) decision is one scalar bit test of a readlane'd column
-        // (s_bitcmp + s_cbranch) guarding W XORs.  Masked form (small W, where the scalar unit
-        // shared by the CU's waves would be the bottleneck): the U words stay in VGPRs and every
-        // (q, r) costs one v_bfe_i32 mask plus W v_bitop3 (t ^ (cx & mask)), no branches.
+        // cx1[k] = word k+1 of X * window: (cx[k+1] << 1) | (cx[k] >> 31)
+        uint32_t cx1[PAIR ? NX - 1 : 1];
+        if constexpr (PAIR) {
+#pragma unroll
+            for (int k = 0; k < NX - 1; ++k) cx1[k] = funnel(cx[k + 1], cx[k], 31);
+        }
+        // Decision bits, transposed: lane r holds col_r = sum_q bit r of U[q0+q] << q, so each
+        // (q, r) decision is one scalar bit test of a readlane'd column (s_bitcmp + s_cbranch).
         uint32_t colv = 0u;
-        uint32_t uv[MASKED ? QC : 1];
 #pragma unroll
         for (int q = 0; q < QC; ++q) {
             const uint32_t uq = (q0 + q < nu) ? U[q0 + q] : 0u; // uniform address: broadcast read
-            if constexpr (MASKED) uv[q] = uq;
-            else colv |= ((uq >> (lane & 31)) & 1u) << q;
+            colv |= ((uq >> (lane & 31)) & 1u) << q;
         }
 
         uint32_t t[W];
 #pragma unroll
         for (int j = 0; j < W; ++j) t[j] = 0u;
         uint32_t tlo = 0u; // word base-1 (lane 0 only meaningful), MULTI only
-        for (int r = 31; r >= 0; --r) {
-            // t <<= 1 across the whole distributed polynomial
-            const uint32_t prev = wave_shr1(t[W - 1], MULTI ? tlo : 0u);
+        if constexpr (PAIR) {
+            for (int r = 30; r >= 0; r -= 2) {
+                // t <<= 2 across the whole distributed polynomial
+                const uint32_t prev = wave_shr1(t[W - 1], MULTI ? tlo : 0u);
 #pragma unroll
-            for (int j = W - 1; j >= 1; --j) t[j] = funnel(t[j], t[j - 1], 31);
-            t[0] = funnel(t[0], prev, 31);
-            if (MULTI) tlo <<= 1;
-            if constexpr (MASKED) {
+                for (int j = W - 1; j >= 1; --j) t[j] = funnel(t[j], t[j - 1], 30);
+                t[0] = funnel(t[0], prev, 30);
+                if (MULTI) tlo <<= 2;
+                const uint32_t chi = (uint32_t)__builtin_amdgcn_readlane((int)colv, r + 1);
+                const uint32_t clo = (uint32_t)__builtin_amdgcn_readlane((int)colv, r);
 #pragma unroll
                 for (int q = 0; q < QC; ++q) {
-                    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)uv[q], r, 1);
+                    if (chi & (1u << q)) {
+                        if (clo & (1u << q)) {
+                            asm volatile("" ::);
 #pragma unroll
-                    for (int j = 0; j < W; ++j) t[j] = xor_and(t[j], cx[j - q + QC], m);
-                    if (MULTI) tlo = xor_and(tlo, cx[QC - 1 - q], m);
+                            for (int j = 0; j < W; ++j)
+                                t[j] = __builtin_amdgcn_bitop3_b32(t[j], cx[j - q + QC + 1],
+                                                                   cx1[j - q + QC], 0x96); // xor3
+                            if (MULTI) tlo ^= cx[QC - q] ^ cx1[QC - 1 - q];
+                        } else {
+                            asm volatile("" ::);
+#pragma unroll
+                            for (int j = 0; j < W; ++j) t[j] ^= cx1[j - q + QC];
+                            if (MULTI) tlo ^= cx1[QC - 1 - q];
+                        }
+                    } else if (clo & (1u << q)) {
+                        asm volatile("" ::);
+#pragma unroll
+                        for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC + 1];
+                        if (MULTI) tlo ^= cx[QC - q];
+                    }
                 }
-            } else {
+            }
+        } else {
+            for (int r = 31; r >= 0; --r) {
+                // t <<= 1 across the whole distributed polynomial
+                const uint32_t prev = wave_shr1(t[W - 1], MULTI ? tlo : 0u);
+#pragma unroll
+                for (int j = W - 1; j >= 1; --j) t[j] = funnel(t[j], t[j - 1], 31);
+                t[0] = funnel(t[0], prev, 31);
+                if (MULTI) tlo <<= 1;
                 const uint32_t col = (uint32_t)__builtin_amdgcn_readlane((int)colv, r);
 #pragma unroll
                 for (int q = 0; q < QC; ++q) {
                     if (__builtin_expect((col & (1u << q)) != 0, 1)) {
                         asm volatile("" ::);
 #pragma unroll
-                        for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC];
-                        if (MULTI) tlo ^= cx[QC - 1 - q];
+                        for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC + 1];
+                        if (MULTI) tlo ^= cx[QC - q];
                     }
                 }
             }
@@ -174,17 +207,19 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
     return wave_top_ordered(ldeg);
 }
 
-// Tile widths up to this use the masked (branch-free) decision form.
-constexpr int kMaskedMaxW = 0; // measured: the masked form lost at every width tried
+// Two-bit Horner steps (PAIR) for every tile width; the one-bit form stays for A/B timing.
+#ifndef HM_PAIR
+#define HM_PAIR 0
+#endif
+constexpr bool kPair = HM_PAIR != 0;
 
 template <int QC, int W, int WMAX, bool PAD>
 __device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32_t *V, int nv,
                                          const uint32_t *Add, int nadd, uint32_t *Dst, int nout) {
-    constexpr bool kMasked = W <= kMaskedMaxW;
-    int top = mul_tile<W, QC, false, kMasked, PAD>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
+    int top = mul_tile<W, QC, false, kPair, PAD>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
     if constexpr (W == WMAX && !PAD) { // only the widest tile ever needs more than one pass
         for (int base = kWave * W; base < nout; base += kWave * W) {
-            int t = mul_tile<W, QC, true, kMasked, false>(U, nu, V, nv, Add, nadd, Dst, nout, base);
+            int t = mul_tile<W, QC, true, kPair, false>(U, nu, V, nv, Add, nadd, Dst, nout, base);
             if (t >= 0) top = t;
         }
     }

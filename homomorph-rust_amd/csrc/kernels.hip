@@ -171,88 +171,87 @@ __device__ __forceinline__ uint32_t clmul_word(const uint32_t *__restrict__ pu, 
 __device__ __forceinline__ int bitwords(int degp1) { return degp1 ? ((degp1 - 1) >> 5) + 1 : 0; }
 
 // ---------------------------------------------------------------------------------------------
-// Fused ripple-carry adder, one wavefront per value.  Per bit i (common.rs:43-53):
+// Ripple-carry adder (common.rs:37-56).  Per bit i (common.rs:43-53):
 //   x = a_i ^ b_i;  s_i = x ^ carry;
 //   carry' = (x & carry) ^ (a_i & b_i) & ((x & carry) ^ 1)
 //          = ab_i ^ P_i * carry,   ab_i = a_i b_i,   P_i = x (1 ^ ab_i)   (GF(2)[X] ring identity)
-// ab_i and P_i do not depend on the carry, so they are all computed up front by a SIMT pre-phase
-// in which lanes work on different bits (branch-free per-lane products).  The sequential chain
-// then costs ONE product per bit, P_i * carry, with P_i wave-uniform (scalar branches over its
-// bits, Horner over bit positions) and the carry resident in LDS for the whole chain.
-template <int WMAX, bool PAD>
-__global__ void __launch_bounds__(256) add_kernel(AddArgs A) {
+// ab_i and P_i do not depend on the carry: add_prep_kernel computes all of them in parallel
+// (several waves per value, lanes over (bit, output word), branch-free per-lane products), then
+// add_chain_kernel runs the sequential chain with ONE product per bit, P_i * carry, where P_i is
+// wave-uniform (scalar loads, scalar branches over its bits, Horner over bit positions) and the
+// carry stays in LDS for the whole chain.
+
+__device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
+    uint32_t o = 0;
+    for (uint32_t j = 0; j < i; ++j) o += cap_of(B.b[j]);
+    return o;
+}
+
+__global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
-    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
-    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (e >= A.n) return; // whole wave exits together
+    const uint32_t wave = rfl(threadIdx.x >> 6);
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint64_t e = gw / A.wpv;
+    const uint32_t part = (uint32_t)(gw % A.wpv);
+    if (e >= A.n) return;
     const int lane = lane_id();
     const uint32_t L = A.nbits;
-    uint32_t *Ls = lds + (size_t)wave * A.lds_per_wave;
-    uint32_t *Pall = Ls + A.oP, *C = Ls + A.oC0, *Cn = Ls + A.oC1;
-    uint32_t *degAB = Ls + A.oDeg, *degP = degAB + L; // stored as degree+1, 0 = null
+    const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits part, part+wpv, ...
+    uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
+    uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *ABl = Bl + bpw * A.cntB;
+    uint32_t *dAB = ABl + bpw * A.cntAB, *dP = dAB + bpw;
     uint32_t *ws = A.ws + e * A.ws_stride;
-    uint32_t *Aall = ws, *Ball = ws + (size_t)L * A.cntA, *ABall = Ball + (size_t)L * A.cntB;
-    const uint64_t *pa = A.a.limbs + e * A.a.stride;
-    const uint64_t *pb = A.b.limbs + e * A.b.stride;
-    uint64_t *po = A.out.limbs + e * A.out.stride;
+    uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L;
+    const uint64_t *pa = A.a.limbs + e * A.a.stride, *pb = A.b.limbs + e * A.b.stride;
     const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
-    uint32_t *dout = A.out.degree + e * L;
 
-    // ---- phase 0: validated, masked inputs into the workspace (word slots per bit), plus an LDS
-    // copy for the pre-phase.  The pre-phase scratch (inputs, ab_i) overlays the carry buffers,
-    // which are not live until the chain starts.
-    uint32_t *Al = C, *Bl = C + (size_t)L * A.cntA, *ABl = Bl + (size_t)L * A.cntB;
-    for (uint32_t i = 0, offa = 0, offb = 0; i < L; ++i) {
-        load_bit(pa + offa, rfl(da[i]), A.ab.b[i], Aall + (size_t)i * A.cntA, A.status);
-        load_bit(pb + offb, rfl(db[i]), A.bb.b[i], Ball + (size_t)i * A.cntB, A.status);
-        offa += cap_of(A.ab.b[i]);
-        offb += cap_of(A.bb.b[i]);
+    // stage + validate this wave's bits (every bit is validated, the last one too)
+    uint32_t nmine = 0;
+    for (uint32_t i = part; i < L; i += A.wpv, ++nmine) {
+        load_bit(pa + limb_off(A.ab, i), rfl(da[i]), A.ab.b[i], Al + nmine * A.cntA, A.status);
+        load_bit(pb + limb_off(A.bb, i), rfl(db[i]), A.bb.b[i], Bl + nmine * A.cntB, A.status);
     }
-    for (uint32_t k = lane; k < 2 * L; k += kWave) degAB[k] = 0u;
-    gsync();
-    for (uint32_t k = lane; k < L * A.cntA; k += kWave) Al[k] = Aall[k];
-    for (uint32_t k = lane; k < L * A.cntB; k += kWave) Bl[k] = Ball[k];
+    for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
-
-    // word count of input bit i (0 = null polynomial); per lane
-    auto in_words = [&](const uint32_t *deg, const uint32_t *slot0, uint32_t cnt, uint32_t i) {
+    // products only for bits < L-1 (the last bit has no outgoing carry)
+    const uint32_t nprod = (A.debug_skip & 1u) ? 0u
+                           : (part < L - 1 ? (L - 2 - part) / A.wpv + 1 : 0u);
+    auto words_in = [&](const uint32_t *deg, const uint32_t *slot, uint32_t i) {
         const uint32_t d = deg[i];
-        if (d == 0) return (slot0[(size_t)i * cnt] & 1u) ? 1 : 0;
+        if (d == 0) return (slot[0] & 1u) ? 1 : 0;
         return (int)(d >> 5) + 1;
     };
 
-    // ---- phase 1: ab_i = a_i * b_i for every bit but the last (lanes over (bit, word))
-    const uint32_t nprod = (A.debug_skip & 1u) ? 0u : L - 1;
+    // phase 1: ab_i
     for (uint32_t f0 = 0; f0 < nprod * A.cntAB; f0 += kWave) {
         const uint32_t f = f0 + lane;
         if (f < nprod * A.cntAB) {
-            const uint32_t i = f / A.cntAB, m = f % A.cntAB;
-            const int na = in_words(da, Al, A.cntA, i), nb = in_words(db, Bl, A.cntB, i);
+            const uint32_t t = f / A.cntAB, m = f % A.cntAB, i = part + t * A.wpv;
+            const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
+            const int na = words_in(da, ai, i), nb = words_in(db, bi, i);
             uint32_t w = 0u;
-            if ((int)m < na + nb) {
-                const uint32_t *ai = Al + (size_t)i * A.cntA, *bi = Bl + (size_t)i * A.cntB;
+            if ((int)m < na + nb)
                 w = na <= nb ? clmul_word(ai, na, bi, nb, (int)m) : clmul_word(bi, nb, ai, na, (int)m);
-            }
-            ABl[(size_t)i * A.cntAB + m] = w;
-            ABall[(size_t)i * A.cntAB + m] = w;
-            if (w) atomicMax(&degAB[i], m * 32 + 32 - __builtin_clz(w));
+            ABl[t * A.cntAB + m] = w;
+            ABg[(size_t)i * A.cntAB + m] = w;
+            if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
         }
     }
-    gsync(); // ab_i in the workspace is read by other lanes in the chain
+    wsync();
 
-    // ---- phase 2: P_i = x_i ^ x_i * ab_i,  x_i = a_i ^ b_i   (into LDS)
+    // phase 2: P_i = x_i ^ x_i * ab_i,  x_i = a_i ^ b_i
     for (uint32_t f0 = 0; f0 < nprod * A.cntP; f0 += kWave) {
         const uint32_t f = f0 + lane;
         if (f < nprod * A.cntP) {
-            const uint32_t i = f / A.cntP, m = f % A.cntP;
-            const uint32_t *ai = Al + (size_t)i * A.cntA, *bi = Bl + (size_t)i * A.cntB;
-            const int na = in_words(da, Al, A.cntA, i), nb = in_words(db, Bl, A.cntB, i);
+            const uint32_t t = f / A.cntP, m = f % A.cntP, i = part + t * A.wpv;
+            const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
+            const int na = words_in(da, ai, i), nb = words_in(db, bi, i);
             const int nx = max(na, nb);
-            const int nab = bitwords((int)degAB[i]);
-            const uint32_t *abi = ABl + (size_t)i * A.cntAB;
+            const int nab = bitwords((int)dAB[t]);
+            const uint32_t *abi = ABl + t * A.cntAB;
             uint32_t w = 0u;
             if ((int)m < nx + nab) {
-                // U = x_i (formed on the fly), V = ab_i
                 uint32_t acc = 0u;
                 const int qlo = max(0, (int)m - nab), qhi = min(nx - 1, (int)m);
                 for (int q = qlo; q <= qhi; ++q) {
@@ -265,56 +264,116 @@ __global__ void __launch_bounds__(256) add_kernel(AddArgs A) {
                 w = acc;
                 if ((int)m < nx) w ^= ((int)m < na ? ai[m] : 0u) ^ ((int)m < nb ? bi[m] : 0u);
             }
-            Pall[(size_t)i * A.cntP + m] = w;
-            if (w) atomicMax(&degP[i], m * 32 + 32 - __builtin_clz(w));
+            Pg[(size_t)i * A.cntP + m] = w;
+            if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
         }
     }
     wsync();
+    for (uint32_t t = lane; t < nprod; t += kWave) {
+        const uint32_t i = part + t * A.wpv;
+        degABg[i] = dAB[t];
+        degPg[i] = dP[t];
+    }
+}
 
-    // ---- phase 3: the carry chain.  The carry buffers (which held the pre-phase scratch) are
-    // zeroed with their halos, so the product's window reads need no bounds checks (PAD).
-    for (uint32_t k = lane; k < 2 * (A.cw + kHalo); k += kWave) Ls[A.oC0 - kHalo + k] = 0u;
+// s_i = a_i ^ b_i ^ carry, read straight from the input limbs (masked at the degrees, which the
+// prep kernel validated) and the LDS carry words; writes the output bit and its exact degree.
+__device__ int store_sum_bit(const uint64_t *pa, uint32_t dga, const uint64_t *pb, uint32_t dgb,
+                             const uint32_t *C, int nc, uint64_t *__restrict__ dst, uint32_t bound,
+                             uint32_t *deg_out, int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int nla = (int)(dga >> 6) + 1, nlb = (int)(dgb >> 6) + 1;
+    const uint64_t ma = (~0ull) >> (63 - (dga & 63)), mb = (~0ull) >> (63 - (dgb & 63));
+    const int total = max(max(cap, max(nla, nlb)), (nc + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        uint64_t v = 0;
+        if (g < nla) v ^= g == nla - 1 ? (pa[g] & ma) : pa[g];
+        if (g < nlb) v ^= g == nlb - 1 ? (pb[g] & mb) : pb[g];
+        const int w = 2 * g;
+        const uint32_t lo = w < nc ? C[w] : 0u, hi = w + 1 < nc ? C[w + 1] : 0u;
+        v ^= (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+template <int WMAX, bool PAD>
+__global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    const uint32_t L = A.nbits;
+    uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
+    uint32_t *C = Ls + kHalo, *Cn = C + A.cw + kHalo;
+    uint32_t *Pl = Cn + A.cw; // P_i slots, copied once from the workspace (uniform reads per step)
+    const uint32_t *ws = A.ws + e * A.ws_stride;
+    const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L;
+    const uint64_t *pa = A.a.limbs + e * A.a.stride, *pb = A.b.limbs + e * A.b.stride;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
+    uint32_t *dout = A.out.degree + e * L;
+
+    // zero both carry buffers with their halos: window reads need no bounds checks (PAD)
+    const uint32_t ncarry = 2 * (A.cw + kHalo);
+    for (uint32_t k = lane; k < ncarry; k += kWave) Ls[k] = 0u;
+    for (uint32_t k = lane; k < (L - 1) * A.cntP; k += kWave) Pl[k] = Pg[k];
     wsync();
     int nc = 0; // carry words (0 = null carry, common.rs:39)
-    uint32_t offo = 0;
+    uint32_t offa = 0, offb = 0, offo = 0;
     for (uint32_t i = 0; i < L; ++i) {
-        const uint32_t *ai = Aall + (size_t)i * A.cntA, *bi = Ball + (size_t)i * A.cntB;
-        const uint32_t dga = rfl(da[i]), dgb = rfl(db[i]);
-        const int na = dga ? (int)(dga >> 5) + 1 : (int)(rfl(ai[0]) & 1u);
-        const int nb = dgb ? (int)(dgb >> 5) + 1 : (int)(rfl(bi[0]) & 1u);
-        store_xor3_bit(ai, na, bi, nb, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
+        store_sum_bit(pa + offa, rfl(da[i]), pb + offb, rfl(db[i]), C, nc, po + offo, A.ob.b[i],
+                      dout + i, A.status);
         if (i + 1 < L && !(A.debug_skip & 2u)) {
-            const int np = bitwords((int)rfl(degP[i])), nab = bitwords((int)rfl(degAB[i]));
+            const int np = bitwords((int)degPg[i]), nab = bitwords((int)degABg[i]);
             int nout;
-            nc = words_of(wave_mul<kQBig, WMAX, PAD>(Pall + (size_t)i * A.cntP, np, C, nc,
-                                                     ABall + (size_t)i * A.cntAB, nab, Cn, &nout));
+            nc = words_of(wave_mul<kQBig, WMAX, PAD>(Pl + (size_t)i * A.cntP, np, C, nc,
+                                                     ABg + (size_t)i * A.cntAB, nab, Cn, &nout));
             wsync();
             uint32_t *t = C;
             C = Cn;
             Cn = t;
         }
+        offa += cap_of(A.ab.b[i]);
+        offb += cap_of(A.bb.b[i]);
         offo += cap_of(A.ob.b[i]);
     }
 }
 
 int launch_add(const AddArgs &a, void *stream) {
+    if (a.n == 0) return 0;
+    // prep: wpv waves per value, 4 waves per block
+    {
+        const uint64_t waves = a.n * a.wpv;
+        const uint64_t blocks = (waves + 3) / 4;
+        hipLaunchKernelGGL(add_prep_kernel, dim3((unsigned)blocks), dim3(256),
+                           (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
     const int wpb = kAddWavesPerBlock;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
-    if (blocks == 0) return 0;
-    const size_t lds = (size_t)a.lds_per_wave * 4 * wpb;
+    const size_t lds = (size_t)a.chain_lds * 4 * wpb;
     // the widest per-lane tile the carry chain needs (carry + P words over 64 lanes)
     const uint32_t need = (a.max_prod_words + 63) / 64;
-    // PAD: every carry product fits one tile of the kernel's widest width, so the zero-padded
-    // carry buffers are read without bounds checks and written whole.
     const bool pad = a.pad != 0;
 #define HM_LAUNCH_ADD(WM)                                                                         \
     do {                                                                                          \
         if (pad)                                                                                  \
-            hipLaunchKernelGGL((add_kernel<WM, true>), dim3((unsigned)blocks), dim3(64 * wpb), lds, \
-                               (hipStream_t)stream, a);                                           \
+            hipLaunchKernelGGL((add_chain_kernel<WM, true>), dim3((unsigned)blocks),              \
+                               dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
         else                                                                                      \
-            hipLaunchKernelGGL((add_kernel<WM, false>), dim3((unsigned)blocks), dim3(64 * wpb),   \
-                               lds, (hipStream_t)stream, a);                                      \
+            hipLaunchKernelGGL((add_chain_kernel<WM, false>), dim3((unsigned)blocks),             \
+                               dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
     } while (0)
     if (need <= 4) HM_LAUNCH_ADD(4);
     else if (need <= 8) HM_LAUNCH_ADD(8);
