@@ -56,26 +56,57 @@ def barrier(world):
         dist.barrier()
 
 
+def broadcast_keys(world, rank, device, sk=None, pk=None, params=PARAMS):
+    """Rank 0's (sk, pk) limbs -> every rank (setup, untimed; RCCL on GPUs, gloo in the CPU
+    tests).  Returns host uint64 arrays (sk: d/64+1 limbs, pk: tau x (d+dp)/64+1 limbs)."""
+    if world == 1:
+        return sk, pk
+    d, dp, delta, tau = params
+    skt = torch.zeros(d // 64 + 1, dtype=torch.int64, device=device)
+    pkt = torch.zeros((tau, (d + dp) // 64 + 1), dtype=torch.int64, device=device)
+    if rank == 0:
+        skt[: len(sk)].copy_(torch.from_numpy(np.ascontiguousarray(sk, np.uint64).view(np.int64)))
+        pk = np.ascontiguousarray(pk, np.uint64)
+        pkt[:, : pk.shape[1]].copy_(torch.from_numpy(pk.view(np.int64)))
+    dist.broadcast(skt, 0)
+    dist.broadcast(pkt, 0)
+    return skt.cpu().numpy().view(np.uint64), pkt.cpu().numpy().view(np.uint64)
+
+
 def make_context(world, rank, device):
     """Keys are generated on rank 0 and broadcast to every rank (setup, untimed)."""
     ctx = H.Context(H.Parameters(*PARAMS), device=device)
+    sk = pk = None
     if rank == 0:
         ctx.seed_rng(0xB0B)
         ctx.generate_secret_key()
         ctx.generate_public_key()
+        sk, pk = ctx.get_secret_key().limbs, ctx.get_public_key().limbs
     if world > 1:
-        d, dp, delta, tau = PARAMS
-        sk = torch.zeros(d // 64 + 1, dtype=torch.int64, device=device)
-        pk = torch.zeros((tau, (d + dp) // 64 + 1), dtype=torch.int64, device=device)
-        if rank == 0:
-            sk.copy_(torch.from_numpy(ctx.get_secret_key().limbs.view(np.int64)))
-            pk.copy_(torch.from_numpy(ctx.get_public_key().limbs.view(np.int64)))
-        dist.broadcast(sk, 0)
-        dist.broadcast(pk, 0)
+        sk, pk = broadcast_keys(world, rank, device, sk, pk)
         if rank != 0:
-            ctx.set_secret_key(H.SecretKey(sk.cpu().numpy().view(np.uint64)))
-            ctx.set_public_key(H.PublicKey(pk.cpu().numpy().view(np.uint64)))
+            ctx.set_secret_key(H.SecretKey(sk))
+            ctx.set_public_key(H.PublicKey(pk))
     return ctx
+
+
+def shard_inputs(rank, n):
+    """This rank's shard of the synthetic batch: n seeded u32 pairs, distinct per rank (the batch
+    is partitioned into independent values, no exchange between ranks)."""
+    rng = np.random.default_rng(1000 + rank)
+    a = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    b = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    return a, b
+
+
+def reduce_over_ranks(world, device, correct, wall):
+    """(sum of correct results, max wall time) over ranks; identity at world 1."""
+    c = torch.tensor([int(correct)], dtype=torch.int64, device=device)
+    w = torch.tensor([float(wall)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    return int(c.item()), float(w.item())
 
 
 def time_loop(fn, steps, warmup, world, stream=None):
@@ -186,9 +217,7 @@ def main():
     ctx = make_context(world, rank, device)
 
     n = args.batch
-    rng = np.random.default_rng(1000 + rank)
-    a = rng.integers(0, 2**32, size=n, dtype=np.uint32)
-    b = rng.integers(0, 2**32, size=n, dtype=np.uint32)
+    a, b = shard_inputs(rank, n)
     gen = torch.Generator(device=device)
     gen.manual_seed(31 + rank)
     ca, cb = ctx.encrypt(a, generator=gen), ctx.encrypt(b, generator=gen)
@@ -201,12 +230,7 @@ def main():
     ctx.synchronize()  # raises on any device-side error flag
     # verification (untimed): decrypt and compare; digests reduced over RCCL
     dec = ctx.decrypt(out)
-    correct = torch.tensor([int(np.sum(dec == (a + b).astype(np.uint32)))], device=device)
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(correct, op=dist.ReduceOp.SUM)
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall = float(wall_t.item())
+    correct, wall = reduce_over_ranks(world, device, np.sum(dec == (a + b).astype(np.uint32)), wall)
     total = n * world * args.steps
 
     in_bytes = 8 * (ca.stride + cb.stride)
@@ -239,7 +263,7 @@ def main():
         "config": {"workload": "u32 homomorphic add (configs[1])", "global_batch": n * world,
                    "batch_per_gpu": n, "d": PARAMS[0], "dp": PARAMS[1], "delta": PARAMS[2],
                    "tau": PARAMS[3], "parallelism": f"batch-sharded x{world}"},
-        "verified": {"correct_sums": int(correct.item()), "of": n * world},
+        "verified": {"correct_sums": correct, "of": n * world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": 1e3 * kernel_s, "alg_bytes_per_add": per_add,

@@ -53,6 +53,15 @@ __device__ __forceinline__ uint32_t xor_and(uint32_t acc, uint32_t x, uint32_t m
     return __builtin_amdgcn_bitop3_b32(x, acc, m, 0x6c);
 }
 
+// in-place t ^= a and t ^= a ^ b, tied so the register allocator keeps t where it is (the
+// two-bit Horner loop otherwise copies every updated word back after each XOR)
+__device__ __forceinline__ void xor_in(uint32_t &t, uint32_t a) {
+    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(t) : "v"(a));
+}
+__device__ __forceinline__ void xor3_in(uint32_t &t, uint32_t a, uint32_t b) {
+    asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(t) : "v"(a), "v"(b));
+}
+
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -91,7 +100,7 @@ __device__ __forceinline__ int wave_top_ordered(int ldeg) {
 //   folded with one v_bitop3 xor3, so the XOR work per pair drops from 1.0 W to 0.75 W on average,
 //   and the half-rate v_alignbit shifts run once per pair instead of once per bit.
 // Returns the tile's highest set bit index (global), or -1.
-template <int W, int QC, bool MULTI, bool PAIR, bool PAD>
+template <int W, int QC, bool MULTI, int PAIR, bool PAD>
 __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
                                         const uint32_t *__restrict__ V, int nv,
                                         const uint32_t *__restrict__ Add, int nadd,
@@ -101,12 +110,14 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
     nout = (int)rfl((uint32_t)nout), base = (int)rfl((uint32_t)base);
     const int lane = lane_id_local();
     const int w0 = base + lane * W;
+    // PAD: the host guarantees nu <= QC, so there is exactly one chunk and Add is folded in after
+    // it (W fewer registers live across the Horner loop)
     uint32_t acc[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) acc[j] = (w0 + j < nadd) ? Add[w0 + j] : 0u;
+    for (int j = 0; j < W; ++j) acc[j] = (!PAD && w0 + j < nadd) ? Add[w0 + j] : 0u;
 
     const int tile_end = base + kWave * W; // exclusive
-    for (int q0 = 0; q0 < nu; q0 += QC) {
+    for (int q0 = 0; q0 < (PAD ? 1 : nu); q0 += QC) {
         // U chunk words [q0, q0+QC) reach output words [q0, q0 + QC + nv)
         if (q0 >= tile_end || base >= q0 + QC + nv) continue;
         // window: cx[k] = V[w0 - q0 - QC - 1 + k], k in [0, W+QC+1); the word for (j, q) is
@@ -149,26 +160,25 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
                 if (MULTI) tlo <<= 2;
                 const uint32_t chi = (uint32_t)__builtin_amdgcn_readlane((int)colv, r + 1);
                 const uint32_t clo = (uint32_t)__builtin_amdgcn_readlane((int)colv, r);
+                // three exclusive scalar masks and three flat ifs: a nested if/else is
+                // structurised into VCC branches plus register copies
+                const uint32_t both = PAIR == 1 ? chi & clo : 0u;
+                const uint32_t hi = PAIR == 1 ? chi & ~clo : chi, lo = PAIR == 1 ? clo & ~chi : clo;
 #pragma unroll
                 for (int q = 0; q < QC; ++q) {
-                    if (chi & (1u << q)) {
-                        if (clo & (1u << q)) {
-                            asm volatile("" ::);
+                    if (PAIR == 1 && __builtin_expect((both & (1u << q)) != 0, 1)) {
 #pragma unroll
-                            for (int j = 0; j < W; ++j)
-                                t[j] = __builtin_amdgcn_bitop3_b32(t[j], cx[j - q + QC + 1],
-                                                                   cx1[j - q + QC], 0x96); // xor3
-                            if (MULTI) tlo ^= cx[QC - q] ^ cx1[QC - 1 - q];
-                        } else {
-                            asm volatile("" ::);
+                        for (int j = 0; j < W; ++j) xor3_in(t[j], cx[j - q + QC + 1], cx1[j - q + QC]);
+                        if (MULTI) tlo ^= cx[QC - q] ^ cx1[QC - 1 - q];
+                    }
+                    if (__builtin_expect((hi & (1u << q)) != 0, 1)) {
 #pragma unroll
-                            for (int j = 0; j < W; ++j) t[j] ^= cx1[j - q + QC];
-                            if (MULTI) tlo ^= cx1[QC - 1 - q];
-                        }
-                    } else if (clo & (1u << q)) {
-                        asm volatile("" ::);
+                        for (int j = 0; j < W; ++j) xor_in(t[j], cx1[j - q + QC]);
+                        if (MULTI) tlo ^= cx1[QC - 1 - q];
+                    }
+                    if (__builtin_expect((lo & (1u << q)) != 0, 1)) {
 #pragma unroll
-                        for (int j = 0; j < W; ++j) t[j] ^= cx[j - q + QC + 1];
+                        for (int j = 0; j < W; ++j) xor_in(t[j], cx[j - q + QC + 1]);
                         if (MULTI) tlo ^= cx[QC - q];
                     }
                 }
@@ -196,6 +206,10 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
 #pragma unroll
         for (int j = 0; j < W; ++j) acc[j] ^= t[j];
     }
+    if constexpr (PAD) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc[j] ^= (w0 + j < nadd) ? Add[w0 + j] : 0u;
+    }
     int ldeg = -1;
 #pragma unroll
     for (int j = 0; j < W; ++j) {
@@ -207,11 +221,12 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
     return wave_top_ordered(ldeg);
 }
 
-// Two-bit Horner steps (PAIR) for every tile width; the one-bit form stays for A/B timing.
+// Horner step form: 0 = one bit per step; 1 = two bits per step with the both-set case folded
+// into one xor3 (three exclusive tests per word); 2 = two bits per step, two independent tests.
 #ifndef HM_PAIR
-#define HM_PAIR 0
+#define HM_PAIR 2
 #endif
-constexpr bool kPair = HM_PAIR != 0;
+constexpr int kPair = HM_PAIR;
 
 template <int QC, int W, int WMAX, bool PAD>
 __device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32_t *V, int nv,

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libhomomorph_gpu.so")
+# HOMOMORPH_GPU_LIB: an alternative build of the same engine (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("HOMOMORPH_GPU_LIB") or os.path.join(_PKG, "lib", "libhomomorph_gpu.so")
 
 HM_MAX_BITS = 128
 

@@ -1,0 +1,131 @@
+"""Generate the circuit-level golden fixtures under tests/golden/ (run here, on the CPU).
+
+The reference has no circuit-level vectors: its circuits are pinned only by
+decrypt round trips (src/impls/numbers/uint.rs:176-293, src/cipher.rs:275-304).  These fixtures
+are made by the C oracle (oracle/homomorph_oracle.c, the reference's call sequence) from seeded
+keys, masks and plaintexts, and every output polynomial is cross-checked against the independent
+big-int model (oracle/gf2_model.py) before it is written.  The reference itself cannot run here
+(Rust crate, no toolchain), so these pin the GPU path to the oracle, not to the reference binary.
+
+Each case is one .npz (numpy arrays only, no pickles): params, seed, keys, input ciphertexts in
+the batch layout of include/homomorph_gpu.h, the masks that made them, the operation's output,
+and the oracle's decryption of it.
+
+    python tests/golden/make_golden.py      # rewrites tests/golden/*.npz
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "homomorph-rust_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from helpers import as_bytes, bit_ints, fresh_bound, masks, plain  # noqa: E402
+from oracle import gf2_model as model  # noqa: E402
+from oracle import oracle_py as oracle  # noqa: E402
+
+# name: (op, params (d, dp, delta, tau), plaintext dtype, n, key seed)
+CASES = {
+    "add_u8_d64": ("add", (64, 64, 1, 64), np.uint8, 4, 101),
+    "add_u32_d64": ("add", (64, 64, 1, 64), np.uint32, 2, 102),
+    "add_u32_d128": ("add", (128, 128, 1, 128), np.uint32, 4, 103),  # the bench configuration
+    "mul_u8_d128": ("mul", (128, 128, 1, 128), np.uint8, 2, 104),    # benches/u8.rs:9
+    "mul_i8_d512": ("smul", (512, 64, 1, 64), np.int8, 2, 105),      # int.rs:247-268 params
+    "encdec_u32_d128": ("encdec", (128, 128, 1, 128), np.uint32, 8, 106),
+    "and_u8_d32": ("and", (32, 8, 8, 8), np.uint8, 2, 107),          # uint.rs:108-174 params
+    "or_u8_d32": ("or", (32, 8, 8, 8), np.uint8, 2, 108),
+    "xor_u8_d32": ("xor", (32, 16, 16, 16), np.uint8, 2, 109),
+    "not_u8_d32": ("not", (32, 16, 16, 16), np.uint8, 2, 110),
+}
+
+
+def _plain_result(op, a, b, dtype):
+    a64, b64 = a.astype(np.int64), b.astype(np.int64)
+    r = {"add": a64 + b64, "mul": a64 * b64, "smul": a64 * b64, "encdec": a64,
+         "and": a64 & b64, "or": a64 | b64, "xor": a64 ^ b64, "not": ~a64}[op]
+    return r.astype(dtype)
+
+
+def _check_model(op, la, da, lb, db, bound, lo, do, obound, n):
+    for e in range(n):
+        A, B = bit_ints(la, da, bound, e), bit_ints(lb, db, bound, e)
+        if op == "add":
+            ref = model.add_circuit(A, B)
+        elif op in ("mul", "smul"):
+            ref = model.mul_circuit(A, B, signed=op == "smul")
+        elif op == "and":
+            ref = [model.clmul(x, y) for x, y in zip(A, B)]
+        elif op == "xor":
+            ref = [x ^ y for x, y in zip(A, B)]
+        elif op == "or":
+            ref = [x ^ y ^ model.clmul(x, y) for x, y in zip(A, B)]
+        elif op == "not":
+            ref = [x ^ 1 for x in A]
+        else:
+            raise ValueError(op)
+        got = bit_ints(lo, do, obound, e)
+        assert got == ref, f"{op}: oracle != model at value {e}"
+        degs = np.asarray(do, dtype=np.int64).reshape(n, -1)[e]
+        assert [model.degree(x) for x in ref] == degs.tolist()
+
+
+def make(name):
+    import homomorph as H
+    op, params, dtype, n, seed = CASES[name]
+    d, dp, delta, tau = params
+    sk, pk, pkdeg = oracle.keygen(d, dp, delta, tau, seed)
+    s, T = model.keygen(d, dp, delta, tau, seed)
+    assert model.limbs_to_int(sk) == s and [model.limbs_to_int(r) for r in pk] == T
+    nbits = 8 * np.dtype(dtype).itemsize
+    a, b = plain(n, dtype, seed + 1), plain(n, dtype, seed + 2)
+    ma, mb = masks(n, nbits, tau, seed + 3), masks(n, nbits, tau, seed + 4)
+    bound = fresh_bound(d, dp, nbits)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    ab = as_bytes(a)
+    for e in range(n):  # encryption vs the model, bit by bit (bit k = bit k%8 of byte k/8)
+        A = bit_ints(la, da, bound, e)
+        for k in range(nbits):
+            x = (int(ab[e, k // 8]) >> (k % 8)) & 1
+            assert A[k] == model.cipher_bit(x, T, bytes(ma[e, k]))
+    out = dict(params=np.array(params, dtype=np.uint32), seed=np.array(seed), sk=sk, pk=pk,
+               pk_degree=np.asarray(pkdeg, dtype=np.uint32), a_plain=a, b_plain=b,
+               a_masks=ma, b_masks=mb, in_bound=bound, a_limbs=la, a_degree=da,
+               b_limbs=lb, b_degree=db, op=np.array(op))
+    if op == "encdec":
+        dec = oracle.decrypt_batch(sk, la, da, bound, nbits, n).view(dtype).reshape(-1)
+        out.update(out_bound=bound, out_limbs=la, out_degree=da, out_plain=dec,
+                   expected_plain=a)
+    else:
+        if op == "add":
+            ob = H.add_out_bounds(bound, bound)
+            lo, do = oracle.add_batch(la, da, bound, lb, db, bound, nbits, n, ob)
+        elif op in ("mul", "smul"):
+            ob = H.mul_out_bounds(bound, bound, signed=op == "smul")
+            lo, do = oracle.mul_batch(la, da, bound, lb, db, bound, nbits, n, ob,
+                                      signed=op == "smul")
+        else:
+            opcls = {"and": H.HomomorphicAndGate, "or": H.HomomorphicOrGate,
+                     "xor": H.HomomorphicXorGate, "not": H.HomomorphicNotGate}[op]
+            ob = H.gate_out_bounds(opcls, bound, bound)
+            lo, do = oracle.gate_batch(op, la, da, bound, lb, db, bound, nbits, n, ob)
+        _check_model(op, la, da, lb, db, bound, lo, do, ob, n)
+        dec = oracle.decrypt_batch(sk, lo, do, ob, nbits, n).view(dtype).reshape(-1)
+        out.update(out_bound=ob, out_limbs=lo, out_degree=do, out_plain=dec,
+                   expected_plain=_plain_result(op, a, b, dtype))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    ok = int(np.sum(out["out_plain"] == out["expected_plain"]))
+    print(f"{name}: {os.path.getsize(path)} B, decrypts correctly for {ok}/{n}")
+
+
+if __name__ == "__main__":
+    oracle.build()
+    for name in (sys.argv[1:] or CASES):
+        make(name)

@@ -1,0 +1,96 @@
+"""Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py).
+
+CPU: the oracle regenerates every fixture bit for bit from its seed (keygen RNG contract,
+encryption with the stored masks, the circuit, the decryption).
+GPU: the HIP engine, fed the fixture's keys and input ciphertexts through the C ABI, reproduces
+the stored outputs bit for bit (and encrypts the stored masks to the stored ciphertexts).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from helpers import as_bytes, assert_batches_equal
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = sorted(os.path.splitext(os.path.basename(p))[0]
+                  for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def nbits_n(g):
+    return int(g["in_bound"].size), int(g["a_plain"].size)
+
+
+def test_fixtures_present():
+    assert len(FIXTURES) >= 10, FIXTURES
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_oracle_reproduces_golden(oracle, name):
+    g = load(name)
+    d, dp, delta, tau = (int(x) for x in g["params"])
+    sk, pk, pkdeg = oracle.keygen(d, dp, delta, tau, int(g["seed"]))
+    assert np.array_equal(sk, g["sk"]) and np.array_equal(pk, g["pk"])
+    assert np.array_equal(np.asarray(pkdeg, dtype=np.uint32), g["pk_degree"])
+    nbits, n = nbits_n(g)
+    bound = g["in_bound"]
+    la, da = oracle.encrypt_batch(pk, as_bytes(g["a_plain"]), g["a_masks"], bound)
+    assert_batches_equal(la, da, g["a_limbs"], g["a_degree"], bound, n, name + " encrypt a")
+    lb, db = oracle.encrypt_batch(pk, as_bytes(g["b_plain"]), g["b_masks"], bound)
+    assert_batches_equal(lb, db, g["b_limbs"], g["b_degree"], bound, n, name + " encrypt b")
+    op, ob = str(g["op"]), g["out_bound"]
+    if op == "add":
+        lo, do = oracle.add_batch(la, da, bound, lb, db, bound, nbits, n, ob)
+    elif op in ("mul", "smul"):
+        lo, do = oracle.mul_batch(la, da, bound, lb, db, bound, nbits, n, ob, signed=op == "smul")
+    elif op == "encdec":
+        lo, do = la, da
+    else:
+        lo, do = oracle.gate_batch(op, la, da, bound, lb, db, bound, nbits, n, ob)
+    assert_batches_equal(lo, do, g["out_limbs"], g["out_degree"], ob, n, name + " " + op)
+    dec = oracle.decrypt_batch(sk, lo, do, ob, nbits, n).reshape(-1)
+    assert np.array_equal(dec, g["out_plain"].view(np.uint8).reshape(-1))
+    assert np.array_equal(g["out_plain"], g["expected_plain"])  # the scheme decrypts correctly
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FIXTURES)
+def test_gpu_reproduces_golden(name):
+    import homomorph as H
+    g = load(name)
+    d, dp, delta, tau = (int(x) for x in g["params"])
+    nbits, n = nbits_n(g)
+    ctx = H.Context(H.Parameters(d, dp, delta, tau), device="cuda:0")
+    ctx.set_secret_key(H.SecretKey(g["sk"]))
+    ctx.set_public_key(H.PublicKey(g["pk"]))
+    dtype = g["a_plain"].dtype
+    bound = g["in_bound"]
+    enc = ctx.encrypt(g["a_plain"], masks=g["a_masks"])
+    gl, gd = enc.to_host()
+    assert_batches_equal(gl, gd, g["a_limbs"], g["a_degree"], bound, n, name + " gpu encrypt")
+    a = H.Ciphered.from_host(g["a_limbs"], g["a_degree"], bound, n, "cuda:0", dtype)
+    b = H.Ciphered.from_host(g["b_limbs"], g["b_degree"], bound, n, "cuda:0", dtype)
+    op = str(g["op"])
+    if op == "encdec":
+        out = a
+    elif op == "add":
+        out = ctx.apply2(H.HomomorphicAddition, a, b)
+    elif op in ("mul", "smul"):
+        out = ctx.apply2(H.HomomorphicMultiplication, a, b, signed=op == "smul")
+    elif op == "not":
+        out = ctx.apply1(H.HomomorphicNotGate, a)
+    else:
+        opcls = {"and": H.HomomorphicAndGate, "or": H.HomomorphicOrGate,
+                 "xor": H.HomomorphicXorGate}[op]
+        out = ctx.apply2(opcls, a, b)
+    assert np.array_equal(out.bound, g["out_bound"])
+    ol, od = out.to_host()
+    assert_batches_equal(ol, od, g["out_limbs"], g["out_degree"], out.bound, n, name + " gpu")
+    dec = ctx.decrypt(out, dtype)
+    assert np.array_equal(dec, g["out_plain"])
