@@ -561,16 +561,17 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     if (a->n == 0) return HM_OK;
 
     // Workspace slots (words) and LDS plans, from the static bounds
-    uint32_t cntA = 0, cntB = 0, cntAB = 0, cntP = 0, SC = 2, maxPw = 0;
+    uint32_t cntA = 0, cntB = 0, cntAB = 0, cntP = 0, cntX = 1, SC = 2, maxPw = 0;
     int64_t cb = -1;
     for (uint32_t i = 0; i < L; ++i) {
         const int64_t ba = a->bound[i], bb = b->bound[i];
         cntA = std::max(cntA, 2 * cap_of(a->bound[i]));
         cntB = std::max(cntB, 2 * cap_of(b->bound[i]));
+        cntX = std::max(cntX, words_of_bound(std::max(ba, bb)));
         if (i + 1 < L) {
             const int64_t x = std::max(ba, bb), ab = ba + bb, p = x + ab;
-            cntAB = std::max(cntAB, words_of_bound(ba) + words_of_bound(bb));
-            cntP = std::max(cntP, words_of_bound(x) + words_of_bound(ab));
+            cntAB = std::max(cntAB, words_of_bound(ab));
+            cntP = std::max(cntP, words_of_bound(p));
             maxPw = std::max(maxPw, words_of_bound(p));
             SC = std::max(SC, std::max(words_of_bound(p) + words_of_bound(cb), words_of_bound(ab)) + 2);
             cb = (cb < 0) ? ab : std::max(ab, p + cb);
@@ -579,7 +580,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     cntAB = std::max(cntAB, 1u), cntP = std::max(cntP, 1u);
     auto even = [](uint32_t v) { return (v + 1) & ~1u; };
     AddArgs A{};
-    A.cntA = cntA, A.cntB = cntB, A.cntAB = cntAB, A.cntP = cntP;
+    A.cntA = cntA, A.cntB = cntB, A.cntAB = cntAB, A.cntP = cntP, A.cntX = cntX;
     // prep: enough waves per value to keep the chip busy (bits are dealt round-robin)
     {
         const uint64_t want = (16384 + a->n - 1) / a->n;
@@ -598,11 +599,17 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     uint32_t cw = SC;
     if (A.pad) cw = std::max(cw, 64 * wmax);
     A.cw = even(cw);
-    A.chain_lds = even(2 * (A.cw + kHalo) + (L - 1) * cntP);
+    // staged chain (PAD only): one in-place carry buffer, and everything the chain reads per bit
+    // (x_i, ab_i, P_i, degrees) in LDS, so the loop issues no global loads at all
+    const uint32_t staged_lds =
+        even(A.cw + kHalo + (L - 1) * (cntP + cntAB) + L * cntX + 2 * L);
+    A.staged = A.pad && (size_t)staged_lds * 4 * kAddWavesPerBlock <= 160 * 1024;
+    if (const char *e = getenv("HM_ADD_STAGED")) A.staged = A.staged && atoi(e) != 0;
+    A.chain_lds = A.staged ? staged_lds : even(2 * (A.cw + kHalo) + (L - 1) * cntP);
     A.max_prod_words = SC;
     if ((size_t)A.chain_lds * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
     if (const char *dbg = getenv("HM_DEBUG_SKIP")) A.debug_skip = (uint32_t)atoi(dbg);
-    A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2) + 63) & ~(uint64_t)63;
+    A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
     const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
     DeviceGuard g(c->device);
     if (bytes > c->ws_add_bytes) {

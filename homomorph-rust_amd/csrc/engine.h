@@ -31,9 +31,11 @@ struct AddArgs {
     uint32_t *ws;
     uint64_t ws_stride;               // words per value
     uint32_t cntA, cntB, cntAB, cntP; // slot sizes in words (cntA = 2*max cap of a, ...)
+    uint32_t cntX;                    // words of x_i = a_i ^ b_i (masked at the degrees)
     uint32_t wpv;                     // prep: waves per value (bits are dealt round-robin)
     uint32_t prep_lds;                // prep: LDS words per wave
-    uint32_t chain_lds;               // chain: LDS words per wave (two zero-haloed carry buffers)
+    uint32_t chain_lds;               // chain: LDS words per wave
+    uint32_t staged;                  // chain: x, ab, P and degrees staged in LDS, carry in place
     uint32_t cw;                      // chain: carry buffer words
     uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
     uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)

@@ -102,9 +102,9 @@ __device__ __forceinline__ int wave_top_ordered(int ldeg) {
 // Returns the tile's highest set bit index (global), or -1.
 template <int W, int QC, bool MULTI, int PAIR, bool PAD>
 __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
-                                        const uint32_t *__restrict__ V, int nv,
+                                        const uint32_t *V, int nv,
                                         const uint32_t *__restrict__ Add, int nadd,
-                                        uint32_t *__restrict__ Dst, int nout, int base) {
+                                        uint32_t *Dst, int nout, int base) {
     // sizes are wave-uniform; say so, so every size test below is a scalar branch
     nu = (int)rfl((uint32_t)nu), nv = (int)rfl((uint32_t)nv), nadd = (int)rfl((uint32_t)nadd);
     nout = (int)rfl((uint32_t)nout), base = (int)rfl((uint32_t)base);
@@ -242,7 +242,8 @@ __device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32
 }
 
 // Dst[0..nout) = Add ^ U*V with nout = max(nu+nv, nadd).  Returns the exact degree (-1 = null).
-// Dst must not alias U, V or Add.  The per-lane tile width W is picked from nout among the
+// Dst must not alias U or Add; it may alias V only in PAD mode (one chunk, one tile: every window
+// word is read into registers before the tile is written).  The per-lane tile width W is picked from nout among the
 // instantiated widths <= WMAX (the kernel's VGPR budget is set by WMAX + QC); longer outputs are
 // produced in several WMAX-wide tiles.
 // PAD (caller guarantees): V has >= kHalo zero words below it and zeros from nv up to 64*WMAX,

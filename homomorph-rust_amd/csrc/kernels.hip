@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     uint32_t *dAB = ABl + bpw * A.cntAB, *dP = dAB + bpw;
     uint32_t *ws = A.ws + e * A.ws_stride;
     uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
-    uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L;
+    uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
     const uint64_t *pa = A.a.limbs + e * A.a.stride, *pb = A.b.limbs + e * A.b.stride;
     const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
 
@@ -222,6 +222,14 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
         if (d == 0) return (slot[0] & 1u) ? 1 : 0;
         return (int)(d >> 5) + 1;
     };
+
+    // x_i = a_i ^ b_i for every bit (the chain's sum bits read it instead of the raw limbs)
+    for (uint32_t f = lane; f < nmine * A.cntX; f += kWave) {
+        const uint32_t t = f / A.cntX, m = f % A.cntX, i = part + t * A.wpv;
+        const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
+        const int na = words_in(da, ai, i), nb = words_in(db, bi, i);
+        Xg[(size_t)i * A.cntX + m] = ((int)m < na ? ai[m] : 0u) ^ ((int)m < nb ? bi[m] : 0u);
+    }
 
     // phase 1: ab_i
     for (uint32_t f0 = 0; f0 < nprod * A.cntAB; f0 += kWave) {
@@ -350,6 +358,75 @@ __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
     }
 }
 
+// Staged chain (PAD plans whose slots fit in LDS).  Everything the loop reads per bit -- x_i,
+// ab_i, P_i and the product degrees -- is copied from the workspace into LDS once, and the carry
+// is updated in place (PAD products read their whole window before writing their tile), so the
+// only global traffic inside the loop is the output stores: no load ever waits behind them.
+__device__ int store_sum_x(const uint32_t *X, int nx, const uint32_t *C, int nc,
+                           uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
+                           int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int total = max(cap, (max(nx, nc) + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        const uint32_t lo = (w < nx ? X[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        const uint32_t hi = (w + 1 < nx ? X[w + 1] : 0u) ^ (w + 1 < nc ? C[w + 1] : 0u);
+        const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+template <int WMAX>
+__global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    const uint32_t L = A.nbits;
+    // LDS: [halo][C: cw][P: (L-1) cntP][AB: (L-1) cntAB][X: L cntX][degP: L][degAB: L]
+    uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
+    uint32_t *C = Ls + kHalo;
+    uint32_t *Pl = C + A.cw, *ABl = Pl + (size_t)(L - 1) * A.cntP;
+    uint32_t *Xl = ABl + (size_t)(L - 1) * A.cntAB, *dPl = Xl + (size_t)L * A.cntX, *dABl = dPl + L;
+    const uint32_t *ws = A.ws + e * A.ws_stride;
+    const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    uint32_t *dout = A.out.degree + e * L;
+
+    for (uint32_t k = lane; k < kHalo + A.cw; k += kWave) Ls[k] = 0u;
+    for (uint32_t k = lane; k < (L - 1) * A.cntP; k += kWave) Pl[k] = Pg[k];
+    for (uint32_t k = lane; k < (L - 1) * A.cntAB; k += kWave) ABl[k] = ABg[k];
+    for (uint32_t k = lane; k < L * A.cntX; k += kWave) Xl[k] = Xg[k];
+    for (uint32_t k = lane; k < L; k += kWave) dPl[k] = degPg[k], dABl[k] = degABg[k];
+    wsync();
+    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    uint32_t offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        store_sum_x(Xl + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
+                    A.status);
+        if (i + 1 < L && !(A.debug_skip & 2u)) {
+            const int np = bitwords((int)rfl(dPl[i])), nab = bitwords((int)rfl(dABl[i]));
+            int nout;
+            wsync(); // the sum bit's reads of C precede the in-place product's writes
+            nc = words_of(wave_mul<kQBig, WMAX, true>(Pl + (size_t)i * A.cntP, np, C, nc,
+                                                      ABl + (size_t)i * A.cntAB, nab, C, &nout));
+            wsync();
+        }
+        offo += cap_of(A.ob.b[i]);
+    }
+}
+
 int launch_add(const AddArgs &a, void *stream) {
     if (a.n == 0) return 0;
     // prep: wpv waves per value, 4 waves per block
@@ -368,7 +445,10 @@ int launch_add(const AddArgs &a, void *stream) {
     const bool pad = a.pad != 0;
 #define HM_LAUNCH_ADD(WM)                                                                         \
     do {                                                                                          \
-        if (pad)                                                                                  \
+        if (a.staged)                                                                             \
+            hipLaunchKernelGGL((add_chain_staged_kernel<WM>), dim3((unsigned)blocks),             \
+                               dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
+        else if (pad)                                                                             \
             hipLaunchKernelGGL((add_chain_kernel<WM, true>), dim3((unsigned)blocks),              \
                                dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
         else                                                                                      \
