@@ -1,7 +1,10 @@
 // kernels.hip — gfx950 kernels of the GF(2)[X] homomorphic engine.
 //
-//   add_kernel      fused ripple-carry adder, one wavefront per value, carry chain kept in LDS
-//                   (src/impls/numbers/common.rs:37-56 add_internal)
+//   add_prep_kernel ripple-carry adder, carry-independent part: ab_i, P_i, x_i for every bit,
+//                   lanes over (bit, word), several waves per value
+//   add_chain_staged_kernel / add_chain_kernel
+//                   the carry chain carry' = ab_i ^ P_i * carry, one wavefront per value, carry
+//                   kept in LDS (src/impls/numbers/common.rs:37-56 add_internal)
 //   mul_kernel      carry-save multiplier, one wavefront per value, carries in a global workspace
 //                   (common.rs:66-105 mul_unsigned_internal, :115-155 mul_signed_internal)
 //   gate_kernel     elementwise AND/OR/XOR/NOT (common.rs:5-35)

@@ -182,9 +182,12 @@ hm_status hm_gate_batch(hm_ctx *ctx, hm_op gate, const hm_batch *a, const hm_bat
                         hm_batch *out);
 
 /* ---------------- polynomial primitives (src/polynomial.rs), for unit parity ---------------- */
+/* Polynomial::add (polynomial.rs:190-213) per pair: out = a ^ b, exact degree. */
 hm_status hm_poly_add_batch(hm_ctx *ctx, const hm_polys *a, const hm_polys *b, hm_polys *out);
+/* Polynomial::mul (polynomial.rs:252-310) per pair: carry-less product, null short-circuit. */
 hm_status hm_poly_mul_batch(hm_ctx *ctx, const hm_polys *a, const hm_polys *b, hm_polys *out);
-/* remainder by ONE divisor s (host limbs) for every polynomial of a */
+/* Polynomial::rem (polynomial.rs:316-365): remainder by ONE divisor s (host limbs) for every
+ * polynomial of a; s = 0 -> HM_ERR_DIVIDE_BY_ZERO, s = 1 -> HM_ERR_DIVISOR_IS_ONE. */
 hm_status hm_poly_rem_batch(hm_ctx *ctx, const hm_polys *a, const uint64_t *s_limbs,
                             size_t s_nlimbs, hm_polys *out);
 
