@@ -258,7 +258,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (GF(2)[X] over u64 limbs)",
+        "dtype": "u32",
         "data": "synthetic: seeded u32 plaintexts, seeded keys, device-drawn subset masks",
         "config": {"workload": "u32 homomorphic add (configs[1])", "global_batch": n * world,
                    "batch_per_gpu": n, "d": PARAMS[0], "dp": PARAMS[1], "delta": PARAMS[2],
@@ -267,7 +267,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": 1e3 * kernel_s, "alg_bytes_per_add": per_add,
-                     "note": "VALU-bound carry-less arithmetic; see DESIGN.md for the VALU roofline"},
+                     "kernels": "add_prep_kernel + add_chain_staged_kernel (one launch)",
+                     "note": "issue-bound (VALU + scalar bit decisions), not HBM: DESIGN.md s4"},
     }
     if rank == 0 and world == 1 and not args.no_secondary:
         try:

@@ -137,38 +137,59 @@ constexpr int kQSmall = 10;
 constexpr int kQBig = 25;
 
 // ---------------------------------------------------------------------------------------------
-// Low word of (u * (v1:v0)) >> 0 restricted to the window: XOR over set bits r of u of the
-// funnel-shifted pair (v1 << r | v0 >> (32 - r)).  Four independent accumulators break the
-// dependent bitop3 chain (VALU latency) into four interleaved chains.
-__device__ __forceinline__ uint32_t clmul_word_step(uint32_t u, uint32_t v1, uint32_t v0) {
-    uint32_t a0 = v1 & (0u - (u & 1u)), a1 = 0u, a2 = 0u, a3 = 0u;
+// Per-lane carry-less product word by integer multiplication of "holey" operands.
+// Split u and v by bit position mod 4 (u_a = u & M_a, M_a = 0x11111111 << a).  In the integer
+// product u_a * v_b every set bit pair lands on a position == a+b (mod 4), and at most 8 pairs
+// land on any one position (8 bits per holey word), so the column counts never carry out of
+// their 4-bit field: bit p of u_a*v_b is the GF(2) coefficient sum at p.  XOR the 4 products of
+// each residue class c, keep the positions == c:  clmul(u, v) = OR_c (M_c & XOR_{a+b=c} u_a v_b).
+// v_mul_lo_u32 / v_mul_hi_u32 give the two halves of the 64-bit product at the rate of a shift
+// (measured), i.e. 16 multiplies replace 32 (funnel + bfe + bitop3) bit steps.
+// Masking commutes with XOR, so classes are accumulated over q and masked once per word.
+struct Holey {
+    uint32_t h[4];
+    __device__ __forceinline__ explicit Holey(uint32_t v) {
 #pragma unroll
-    for (int r = 1; r < 32; r += 4) {
-        a1 = xor_and(a1, funnel(v1, v0, 32 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r, 1));
-        a2 = xor_and(a2, funnel(v1, v0, 31 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r + 1, 1));
-        a3 = xor_and(a3, funnel(v1, v0, 30 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r + 2, 1));
-        if (r + 3 < 32)
-            a0 = xor_and(a0, funnel(v1, v0, 29 - r), (uint32_t)__builtin_amdgcn_sbfe((int)u, r + 3, 1));
+        for (int a = 0; a < 4; ++a) h[a] = v & (0x11111111u << a);
     }
-    return a0 ^ a1 ^ a2 ^ a3;
+};
+
+// z[c] ^= low halves of U (x) V1  ^  high halves of U (x) V0   (residue class c)
+__device__ __forceinline__ void holey_acc(uint32_t z[4], const Holey &U, const Holey &V1,
+                                          const Holey &V0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int b = (c - a) & 3;
+            lo ^= U.h[a] * V1.h[b];
+            hi ^= __umulhi(U.h[a], V0.h[b]);
+        }
+        z[c] ^= lo ^ hi;
+    }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Per-lane carry-less product word: word m of U*V (U: nu words, V: nv words).  Branch-free:
-// every bit r of U_q selects (by a sign-extended mask) the funnel-shifted V window.  Used where
-// lanes work on DIFFERENT products (no uniform operand), i.e. the adder's pre-phase.
+__device__ __forceinline__ uint32_t holey_fold(const uint32_t z[4]) {
+    return (z[0] & 0x11111111u) | (z[1] & 0x22222222u) | (z[2] & 0x44444444u) |
+           (z[3] & 0x88888888u);
+}
+
+// Word m of U*V (U: nu words, V: nv words): XOR over q of low(U_q V_{m-q}) ^ high(U_q V_{m-q-1}).
+// Used where lanes work on DIFFERENT products (no uniform operand), i.e. the adder's pre-phase.
 __device__ __forceinline__ uint32_t clmul_word(const uint32_t *__restrict__ pu, int nu,
                                                const uint32_t *__restrict__ pv, int nv, int m) {
-    uint32_t acc = 0u;
+    uint32_t z[4] = {0u, 0u, 0u, 0u};
     const int qlo = max(0, m - nv), qhi = min(nu - 1, m);
-    for (int q = qlo; q <= qhi; ++q) {
-        const uint32_t u = pu[q];
-        const int k = m - q;
-        const uint32_t v1 = k < nv ? pv[k] : 0u;
-        const uint32_t v0 = (k >= 1 && k - 1 < nv) ? pv[k - 1] : 0u;
-        acc ^= clmul_word_step(u, v1, v0);
+    if (qlo > qhi) return 0u;
+    int k = m - qlo;
+    Holey V1(k < nv ? pv[k] : 0u);
+    for (int q = qlo; q <= qhi; ++q, --k) {
+        const Holey V0((k >= 1 && k - 1 < nv) ? pv[k - 1] : 0u);
+        holey_acc(z, Holey(pu[q]), V1, V0);
+        V1 = V0; // V_{m-q-1} is the next q's V_{m-q}
     }
-    return acc;
+    return holey_fold(z);
 }
 
 __device__ __forceinline__ int bitwords(int degp1) { return degp1 ? ((degp1 - 1) >> 5) + 1 : 0; }
@@ -200,9 +221,11 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const int lane = lane_id();
     const uint32_t L = A.nbits;
     const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits part, part+wpv, ...
+    // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][na nb dAB dP: 4 bpw]
     uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
-    uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *ABl = Bl + bpw * A.cntB;
-    uint32_t *dAB = ABl + bpw * A.cntAB, *dP = dAB + bpw;
+    uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
+    uint32_t *ABl = Xl + bpw * A.cntX;
+    uint32_t *nAl = ABl + bpw * A.cntAB, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
     uint32_t *ws = A.ws + e * A.ws_stride;
     uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
     uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
@@ -212,71 +235,66 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     // stage + validate this wave's bits (every bit is validated, the last one too)
     uint32_t nmine = 0;
     for (uint32_t i = part; i < L; i += A.wpv, ++nmine) {
-        load_bit(pa + limb_off(A.ab, i), rfl(da[i]), A.ab.b[i], Al + nmine * A.cntA, A.status);
-        load_bit(pb + limb_off(A.bb, i), rfl(db[i]), A.bb.b[i], Bl + nmine * A.cntB, A.status);
+        const int na = load_bit(pa + limb_off(A.ab, i), rfl(da[i]), A.ab.b[i], Al + nmine * A.cntA,
+                                A.status);
+        const int nb = load_bit(pb + limb_off(A.bb, i), rfl(db[i]), A.bb.b[i], Bl + nmine * A.cntB,
+                                A.status);
+        if (lane == 0) nAl[nmine] = (uint32_t)na, nBl[nmine] = (uint32_t)nb;
     }
     for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
     // products only for bits < L-1 (the last bit has no outgoing carry)
     const uint32_t nprod = (A.debug_skip & 1u) ? 0u
                            : (part < L - 1 ? (L - 2 - part) / A.wpv + 1 : 0u);
-    auto words_in = [&](const uint32_t *deg, const uint32_t *slot, uint32_t i) {
-        const uint32_t d = deg[i];
-        if (d == 0) return (slot[0] & 1u) ? 1 : 0;
-        return (int)(d >> 5) + 1;
-    };
 
-    // x_i = a_i ^ b_i for every bit (the chain's sum bits read it instead of the raw limbs)
+    // x_i = a_i ^ b_i for every bit: LDS for the P products, workspace for the chain's sum bits
     for (uint32_t f = lane; f < nmine * A.cntX; f += kWave) {
         const uint32_t t = f / A.cntX, m = f % A.cntX, i = part + t * A.wpv;
-        const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
-        const int na = words_in(da, ai, i), nb = words_in(db, bi, i);
-        Xg[(size_t)i * A.cntX + m] = ((int)m < na ? ai[m] : 0u) ^ ((int)m < nb ? bi[m] : 0u);
+        const int na = (int)nAl[t], nb = (int)nBl[t];
+        const uint32_t x = ((int)m < na ? Al[t * A.cntA + m] : 0u) ^
+                           ((int)m < nb ? Bl[t * A.cntB + m] : 0u);
+        Xl[t * A.cntX + m] = x;
+        Xg[(size_t)i * A.cntX + m] = x;
     }
 
-    // phase 1: ab_i
-    for (uint32_t f0 = 0; f0 < nprod * A.cntAB; f0 += kWave) {
-        const uint32_t f = f0 + lane;
-        if (f < nprod * A.cntAB) {
-            const uint32_t t = f / A.cntAB, m = f % A.cntAB, i = part + t * A.wpv;
-            const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
-            const int na = words_in(da, ai, i), nb = words_in(db, bi, i);
-            uint32_t w = 0u;
-            if ((int)m < na + nb)
-                w = na <= nb ? clmul_word(ai, na, bi, nb, (int)m) : clmul_word(bi, nb, ai, na, (int)m);
-            ABl[t * A.cntAB + m] = w;
-            ABg[(size_t)i * A.cntAB + m] = w;
-            if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
+    // phase 1: ab_i.  Lanes over (slot t, word m); (t, m) advance incrementally per pass.
+    {
+        const uint32_t cnt = A.cntAB, dt = kWave / cnt, dm = kWave % cnt;
+        uint32_t t = (uint32_t)lane / cnt, m = (uint32_t)lane % cnt;
+        for (uint32_t f0 = 0; f0 < nprod * cnt; f0 += kWave) {
+            if (t < nprod) {
+                const uint32_t i = part + t * A.wpv;
+                const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
+                const int na = (int)nAl[t], nb = (int)nBl[t];
+                const uint32_t w = (int)m < na + nb ? clmul_word(ai, na, bi, nb, (int)m) : 0u;
+                ABl[t * cnt + m] = w;
+                ABg[(size_t)i * cnt + m] = w;
+                if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
+            }
+            t += dt, m += dm;
+            if (m >= cnt) m -= cnt, ++t;
         }
     }
     wsync();
 
-    // phase 2: P_i = x_i ^ x_i * ab_i,  x_i = a_i ^ b_i
-    for (uint32_t f0 = 0; f0 < nprod * A.cntP; f0 += kWave) {
-        const uint32_t f = f0 + lane;
-        if (f < nprod * A.cntP) {
-            const uint32_t t = f / A.cntP, m = f % A.cntP, i = part + t * A.wpv;
-            const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
-            const int na = words_in(da, ai, i), nb = words_in(db, bi, i);
-            const int nx = max(na, nb);
-            const int nab = bitwords((int)dAB[t]);
-            const uint32_t *abi = ABl + t * A.cntAB;
-            uint32_t w = 0u;
-            if ((int)m < nx + nab) {
-                uint32_t acc = 0u;
-                const int qlo = max(0, (int)m - nab), qhi = min(nx - 1, (int)m);
-                for (int q = qlo; q <= qhi; ++q) {
-                    const uint32_t u = (q < na ? ai[q] : 0u) ^ (q < nb ? bi[q] : 0u);
-                    const int k = (int)m - q;
-                    const uint32_t v1 = k < nab ? abi[k] : 0u;
-                    const uint32_t v0 = (k >= 1 && k - 1 < nab) ? abi[k - 1] : 0u;
-                    acc ^= clmul_word_step(u, v1, v0);
-                }
-                w = acc;
-                if ((int)m < nx) w ^= ((int)m < na ? ai[m] : 0u) ^ ((int)m < nb ? bi[m] : 0u);
+    // phase 2: P_i = x_i ^ x_i * ab_i
+    {
+        const uint32_t cnt = A.cntP, dt = kWave / cnt, dm = kWave % cnt;
+        uint32_t t = (uint32_t)lane / cnt, m = (uint32_t)lane % cnt;
+        for (uint32_t f0 = 0; f0 < nprod * cnt; f0 += kWave) {
+            if (t < nprod) {
+                const uint32_t i = part + t * A.wpv;
+                const uint32_t *xi = Xl + t * A.cntX;
+                const int nx = max((int)nAl[t], (int)nBl[t]);
+                const int nab = bitwords((int)dAB[t]);
+                uint32_t w = (int)m < nx + nab ? clmul_word(xi, nx, ABl + t * A.cntAB, nab, (int)m)
+                                               : 0u;
+                if ((int)m < nx) w ^= xi[m];
+                Pg[(size_t)i * cnt + m] = w;
+                if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
             }
-            Pg[(size_t)i * A.cntP + m] = w;
-            if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
+            t += dt, m += dm;
+            if (m >= cnt) m -= cnt, ++t;
         }
     }
     wsync();
