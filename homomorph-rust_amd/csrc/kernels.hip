@@ -192,6 +192,33 @@ __device__ __forceinline__ uint32_t clmul_word(const uint32_t *__restrict__ pu, 
     return holey_fold(z);
 }
 
+// One row of a product: out[k] ^= word k of u * V for k = 0..nv (out in LDS, shared by the
+// lanes that own the other rows, hence ds_xor).  Each 32x32 product is formed whole: 16
+// v_mad_u64_u32 give both halves, the low half goes to word k and the high half to word k+1.
+__device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__restrict__ pv, int nv,
+                                              uint32_t *out) {
+    const Holey U(u);
+    uint32_t hiprev = 0u;
+    for (int k = 0; k <= nv; ++k) {
+        uint32_t lo = 0u, hi = 0u;
+        if (k < nv) {
+            const Holey V(pv[k]);
+            uint64_t z[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) z[(a + b) & 3] ^= (uint64_t)U.h[a] * V.h[b];
+            uint32_t zl[4], zh[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) zl[c] = (uint32_t)z[c], zh[c] = (uint32_t)(z[c] >> 32);
+            lo = holey_fold(zl), hi = holey_fold(zh);
+        }
+        const uint32_t w = lo ^ hiprev;
+        if (w) atomicXor(&out[k], w);
+        hiprev = hi;
+    }
+}
+
 __device__ __forceinline__ int bitwords(int degp1) { return degp1 ? ((degp1 - 1) >> 5) + 1 : 0; }
 
 // ---------------------------------------------------------------------------------------------
@@ -221,11 +248,11 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const int lane = lane_id();
     const uint32_t L = A.nbits;
     const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits part, part+wpv, ...
-    // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][na nb dAB dP: 4 bpw]
+    // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][P: bpw cntP][na nb dAB dP]
     uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
     uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
-    uint32_t *ABl = Xl + bpw * A.cntX;
-    uint32_t *nAl = ABl + bpw * A.cntAB, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
+    uint32_t *ABl = Xl + bpw * A.cntX, *Pl = ABl + bpw * A.cntAB;
+    uint32_t *nAl = Pl + bpw * A.cntP, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
     uint32_t *ws = A.ws + e * A.ws_stride;
     uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
     uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
@@ -257,45 +284,47 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
         Xg[(size_t)i * A.cntX + m] = x;
     }
 
-    // phase 1: ab_i.  Lanes over (slot t, word m); (t, m) advance incrementally per pass.
-    {
-        const uint32_t cnt = A.cntAB, dt = kWave / cnt, dm = kWave % cnt;
-        uint32_t t = (uint32_t)lane / cnt, m = (uint32_t)lane % cnt;
-        for (uint32_t f0 = 0; f0 < nprod * cnt; f0 += kWave) {
-            if (t < nprod) {
-                const uint32_t i = part + t * A.wpv;
-                const uint32_t *ai = Al + t * A.cntA, *bi = Bl + t * A.cntB;
-                const int na = (int)nAl[t], nb = (int)nBl[t];
-                const uint32_t w = (int)m < na + nb ? clmul_word(ai, na, bi, nb, (int)m) : 0u;
-                ABl[t * cnt + m] = w;
-                ABg[(size_t)i * cnt + m] = w;
-                if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
-            }
-            t += dt, m += dm;
-            if (m >= cnt) m -= cnt, ++t;
+    // Products by rows: lanes over (slot t, multiplier word q) -- every lane of a slot runs the
+    // same number of steps (the multiplicand's length), rows meet in LDS through ds_xor.
+    const uint32_t cq = A.cntX; // multiplier words: a_i (phase 1) and x_i (phase 2) fit in cntX
+    auto for_rows = [&](auto &&row) {
+        const uint32_t dt = kWave / cq, dq = kWave % cq;
+        uint32_t t = (uint32_t)lane / cq, q = (uint32_t)lane % cq;
+        for (uint32_t f0 = 0; f0 < nprod * cq; f0 += kWave) {
+            if (t < nprod) row(t, q);
+            t += dt, q += dq;
+            if (q >= cq) q -= cq, ++t;
         }
+    };
+    // phase 1: ab_i = a_i * b_i
+    for (uint32_t k = lane; k < nprod * A.cntAB; k += kWave) ABl[k] = 0u;
+    for (uint32_t k = lane; k < nprod * A.cntP; k += kWave) Pl[k] = 0u;
+    wsync();
+    for_rows([&](uint32_t t, uint32_t q) {
+        if ((int)q < (int)nAl[t])
+            clmul_row_xor(Al[t * A.cntA + q], Bl + t * A.cntB, (int)nBl[t], ABl + t * A.cntAB + q);
+    });
+    wsync();
+    for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
+        const uint32_t t = f / A.cntAB, m = f % A.cntAB;
+        const uint32_t w = ABl[f];
+        ABg[(size_t)(part + t * A.wpv) * A.cntAB + m] = w;
+        if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
     }
     wsync();
-
     // phase 2: P_i = x_i ^ x_i * ab_i
-    {
-        const uint32_t cnt = A.cntP, dt = kWave / cnt, dm = kWave % cnt;
-        uint32_t t = (uint32_t)lane / cnt, m = (uint32_t)lane % cnt;
-        for (uint32_t f0 = 0; f0 < nprod * cnt; f0 += kWave) {
-            if (t < nprod) {
-                const uint32_t i = part + t * A.wpv;
-                const uint32_t *xi = Xl + t * A.cntX;
-                const int nx = max((int)nAl[t], (int)nBl[t]);
-                const int nab = bitwords((int)dAB[t]);
-                uint32_t w = (int)m < nx + nab ? clmul_word(xi, nx, ABl + t * A.cntAB, nab, (int)m)
-                                               : 0u;
-                if ((int)m < nx) w ^= xi[m];
-                Pg[(size_t)i * cnt + m] = w;
-                if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
-            }
-            t += dt, m += dm;
-            if (m >= cnt) m -= cnt, ++t;
-        }
+    for_rows([&](uint32_t t, uint32_t q) {
+        const int nx = max((int)nAl[t], (int)nBl[t]);
+        if ((int)q < nx)
+            clmul_row_xor(Xl[t * A.cntX + q], ABl + t * A.cntAB, bitwords((int)dAB[t]),
+                          Pl + t * A.cntP + q);
+    });
+    wsync();
+    for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) {
+        const uint32_t t = f / A.cntP, m = f % A.cntP;
+        const uint32_t w = Pl[f] ^ (m < A.cntX ? Xl[t * A.cntX + m] : 0u);
+        Pg[(size_t)(part + t * A.wpv) * A.cntP + m] = w;
+        if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
     }
     wsync();
     for (uint32_t t = lane; t < nprod; t += kWave) {
