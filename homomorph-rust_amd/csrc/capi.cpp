@@ -585,6 +585,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     {
         const uint64_t want = (16384 + a->n - 1) / a->n;
         A.wpv = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 8, (uint64_t)L}));
+        if (const char *w = getenv("HM_PREP_WPV")) A.wpv = std::max(1u, std::min((uint32_t)atoi(w), L));
         const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
         A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 4 * bpw);
         if ((size_t)A.prep_lds * 4 * 4 > 160 * 1024) return HM_ERR_UNSUPPORTED;

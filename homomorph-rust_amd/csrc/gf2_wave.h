@@ -227,14 +227,21 @@ __device__ __forceinline__ int mul_tile(const uint32_t *__restrict__ U, int nu,
 #define HM_PAIR 2
 #endif
 constexpr int kPair = HM_PAIR;
+// Tiles at least this wide are VALU-bound, where folding both-set pairs into one xor3 pays for
+// its extra (taken) scalar branch; narrower tiles are branch-bound and keep two tests per word.
+#ifndef HM_XOR3_MIN_W
+#define HM_XOR3_MIN_W 99
+#endif
+template <int W> constexpr int pair_mode() { return (kPair == 2 && W >= HM_XOR3_MIN_W) ? 1 : kPair; }
 
 template <int QC, int W, int WMAX, bool PAD>
 __device__ __forceinline__ int mul_tiles(const uint32_t *U, int nu, const uint32_t *V, int nv,
                                          const uint32_t *Add, int nadd, uint32_t *Dst, int nout) {
-    int top = mul_tile<W, QC, false, kPair, PAD>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
+    int top = mul_tile<W, QC, false, pair_mode<W>(), PAD>(U, nu, V, nv, Add, nadd, Dst, nout, 0);
     if constexpr (W == WMAX && !PAD) { // only the widest tile ever needs more than one pass
         for (int base = kWave * W; base < nout; base += kWave * W) {
-            int t = mul_tile<W, QC, true, kPair, false>(U, nu, V, nv, Add, nadd, Dst, nout, base);
+            int t = mul_tile<W, QC, true, pair_mode<W>(), false>(U, nu, V, nv, Add, nadd, Dst, nout,
+                                                                 base);
             if (t >= 0) top = t;
         }
     }
