@@ -196,6 +196,18 @@ def secondary_metrics(ctx, device, steps):
     got = ctx.decrypt(co, np.uint8)
     out["u8_mul"] = {"value": n8 * max(1, steps // 4) / wall, "unit": "u8 muls/s", "batch": n8,
                      "verified": bool(np.array_equal(got, (a8.astype(int) * b8) .astype(np.uint8)))}
+
+    # the first 12 result bits of the u32 multiply (the full u32 circuit is
+    # infeasible); bit-exact vs the oracle in tests/test_gpu_parity.py::test_mul_low_parity
+    a32 = np.random.default_rng(3).integers(0, 2**32, size=n8, dtype=np.uint32)
+    b32 = np.random.default_rng(4).integers(0, 2**32, size=n8, dtype=np.uint32)
+    c32a, c32b = ctx.encrypt(a32), ctx.encrypt(b32)
+    ctx.mul_low(c32a, c32b, 12)
+    ctx.synchronize()
+    reps = max(1, steps // 4)
+    wall, _ = time_loop(lambda: ctx.mul_low(c32a, c32b, 12), reps, 0, 1)
+    out["u32_mul_low12"] = {"value": n8 * reps / wall, "unit": "u32 muls/s (result bits 0..11)",
+                            "batch": n8, "verified": "parity test (oracle), not in-bench"}
     return out
 
 

@@ -137,6 +137,7 @@ BatchArg batch_arg(const hm_batch *b) {
     a.limbs = b->limbs;
     a.degree = b->degree;
     a.stride = hm_batch_stride(b->nbits, b->bound);
+    a.dstride = b->nbits;
     return a;
 }
 
@@ -627,16 +628,10 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 
-hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,
-                       hm_batch *out) {
-    if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
-    if (hm_status st = hm_validate_operation(c, is_signed ? HM_OP_MUL_SIGNED : HM_OP_MUL, nullptr); st)
-        return st;
-    for (const hm_batch *x : {a, b, (const hm_batch *)out})
-        if (hm_status st = check_batch(x); st) return st;
-    if (a->nbits != b->nbits || a->nbits != out->nbits || a->n != b->n || a->n != out->n)
-        return HM_ERR_INVALID_ARGUMENT;
-    const uint32_t L = a->nbits;
+// The carry-save multiplier over the low L bits of a and b (L <= their nbits; the limbs are read
+// in place through the batches' own strides).  out has L bits.
+static hm_status mul_impl(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t L,
+                          int is_signed, hm_batch *out) {
     MulPlan P = plan_mul(L, a->bound, b->bound, is_signed);
     if (!P.ok) return HM_ERR_UNSUPPORTED;
     for (uint32_t i = 0; i < L; ++i)
@@ -646,6 +641,7 @@ hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_s
     uint64_t o = 0;
     M.oIn = 0;
     uint64_t wa = 2 * hm_batch_stride(L, a->bound), wb = 2 * hm_batch_stride(L, b->bound);
+    // (only the low L bits are staged: their limbs are the first hm_batch_stride(L) of a value)
     M.in_words_a = (uint32_t)wa;
     o = wa + wb;
     for (uint32_t i = 0; i < L; ++i) {
@@ -676,6 +672,30 @@ hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_s
     fill_bounds(M.ab, a), fill_bounds(M.bb, b), fill_bounds(M.ob, out);
     const uint32_t wpb = 4;
     return launch_mul(M, wpb, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,
+                       hm_batch *out) {
+    if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
+    if (hm_status st = hm_validate_operation(c, is_signed ? HM_OP_MUL_SIGNED : HM_OP_MUL, nullptr); st)
+        return st;
+    for (const hm_batch *x : {a, b, (const hm_batch *)out})
+        if (hm_status st = check_batch(x); st) return st;
+    if (a->nbits != b->nbits || a->nbits != out->nbits || a->n != b->n || a->n != out->n)
+        return HM_ERR_INVALID_ARGUMENT;
+    return mul_impl(c, a, b, a->nbits, is_signed, out);
+}
+
+hm_status hm_mul_low_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t k,
+                           hm_batch *out) {
+    if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
+    if (hm_status st = hm_validate_operation(c, HM_OP_MUL, nullptr); st) return st;
+    for (const hm_batch *x : {a, b, (const hm_batch *)out})
+        if (hm_status st = check_batch(x); st) return st;
+    if (a->nbits != b->nbits || k == 0 || k > a->nbits || out->nbits != k || a->n != b->n ||
+        a->n != out->n)
+        return HM_ERR_INVALID_ARGUMENT;
+    return mul_impl(c, a, b, k, 0, out);
 }
 
 hm_status hm_gate_batch(hm_ctx *c, hm_op gate, const hm_batch *a, const hm_batch *b,

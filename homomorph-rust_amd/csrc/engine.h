@@ -16,7 +16,8 @@ struct Bounds {
 struct BatchArg {
     uint64_t *limbs;
     uint32_t *degree;
-    uint64_t stride; // limbs per value
+    uint64_t stride;  // limbs per value
+    uint32_t dstride; // degree words per value (the batch's nbits; a low-bits view keeps it)
 };
 
 // Fused adder, two launches.  add_prep_kernel (several waves per value, lanes over (bit, word))

@@ -610,8 +610,10 @@ __global__ void __launch_bounds__(256) mul_kernel(MulArgs M) {
         const uint64_t *pa = M.a.limbs + e * M.a.stride, *pb = M.b.limbs + e * M.b.stride;
         uint32_t oa = 0, ob = 0;
         for (uint32_t i = 0; i < L; ++i) {
-            int x = load_bit(pa + oa, rfl(M.a.degree[e * L + i]), M.ab.b[i], Ain + 2 * oa, M.status);
-            int y = load_bit(pb + ob, rfl(M.b.degree[e * L + i]), M.bb.b[i], Bin + 2 * ob, M.status);
+            int x = load_bit(pa + oa, rfl(M.a.degree[e * M.a.dstride + i]), M.ab.b[i], Ain + 2 * oa,
+                             M.status);
+            int y = load_bit(pb + ob, rfl(M.b.degree[e * M.b.dstride + i]), M.bb.b[i], Bin + 2 * ob,
+                             M.status);
             if (lane == 0) na[i] = x, nb[i] = y;
             oa += cap_of(M.ab.b[i]);
             ob += cap_of(M.bb.b[i]);

@@ -501,6 +501,21 @@ class Context:
         self._launch(fn, op.__name__)
         return out
 
+    def mul_low(self, a: Ciphered, b: Ciphered, k: int) -> Ciphered:
+        """Low k bits of HomomorphicMultiplication on a and b: bit-exact
+        equal to the k-bit carry-save circuit on the low k bits (common.rs:66-105), which is how
+        a u32 multiply's first k result bits are obtained when the full u32 circuit is
+        infeasible (its output alone is ~8.4 GiB per value)."""
+        self.validate_operation(HomomorphicMultiplication)
+        if not 1 <= k <= a.nbits:
+            raise ValueError("k must be in 1..nbits")
+        need = mul_out_bounds(a.bound[:k], b.bound[:k])
+        out = Ciphered.empty(a.n, need, self.device, None)
+        ca, cb, co = a._c(), b._c(), out._c()
+        self._launch(lambda: lib().hm_mul_low_batch(self._h, ctypes.byref(ca), ctypes.byref(cb),
+                                                    k, ctypes.byref(co)), "mul_low")
+        return out
+
     def apply1(self, op, a: Ciphered) -> Ciphered:
         """HomomorphicOperation1 (the reference mutates in place; the batch returns a new value)."""
         self.validate_operation(op)

@@ -75,6 +75,8 @@ SIGNATURES = {
     "hm_add_batch": (ctypes.c_int, [vp] + [ctypes.POINTER(HmBatch)] * 3),
     "hm_mul_batch": (ctypes.c_int, [vp, ctypes.POINTER(HmBatch), ctypes.POINTER(HmBatch),
                                     ctypes.c_int, ctypes.POINTER(HmBatch)]),
+    "hm_mul_low_batch": (ctypes.c_int, [vp, ctypes.POINTER(HmBatch), ctypes.POINTER(HmBatch),
+                                        ctypes.c_uint32, ctypes.POINTER(HmBatch)]),
     "hm_gate_batch": (ctypes.c_int, [vp, ctypes.c_int] + [ctypes.POINTER(HmBatch)] * 3),
     "hm_poly_add_batch": (ctypes.c_int, [vp] + [ctypes.POINTER(HmPolys)] * 3),
     "hm_poly_mul_batch": (ctypes.c_int, [vp] + [ctypes.POINTER(HmPolys)] * 3),

@@ -176,6 +176,15 @@ hm_status hm_add_batch(hm_ctx *ctx, const hm_batch *a, const hm_batch *b, hm_bat
  * on first use per size).  Sizes beyond the engine's limits return HM_ERR_UNSUPPORTED. */
 hm_status hm_mul_batch(hm_ctx *ctx, const hm_batch *a, const hm_batch *b, int is_signed,
                        hm_batch *out);
+/* The low k output bits of the nbits-bit multiplier ("u32-mul column
+ * prefix").  Column i of the carry-save circuit (common.rs:66-105) reads input bits <= i and the
+ * carries of columns < i only, so output bits 0..k-1 of the nbits-bit circuit equal the k-bit
+ * circuit on the low k bits, bit for bit.  The signed circuit (:115-155) differs from the
+ * unsigned one only in column nbits-1, so for k < nbits this is also the signed product's low
+ * bits.  a, b: nbits-bit batches read in place; out: k bits, bounds from hm_mul_out_bounds over
+ * the first k input bounds.  Same requirement as HM_OP_MUL (d >= 64 delta). */
+hm_status hm_mul_low_batch(hm_ctx *ctx, const hm_batch *a, const hm_batch *b, uint32_t k,
+                           hm_batch *out);
 /* Context::apply2::<HomomorphicAnd/Or/XorGate> and apply1::<HomomorphicNotGate> (common.rs:5-35,
  * uint.rs:8-58).  For HM_OP_NOT, b is ignored (may be NULL). */
 hm_status hm_gate_batch(hm_ctx *ctx, hm_op gate, const hm_batch *a, const hm_batch *b,

@@ -62,3 +62,12 @@ def assert_batches_equal(l1, d1, l2, d2, bound, n, what=""):
 
 def fresh_bound(d, dp, nbits):
     return np.full(nbits, d + dp, dtype=np.uint32)
+
+
+def low_bits(limbs, deg, bound, n, k):
+    """The low k bit-polynomials of every value of a batch, as a k-bit batch (host copy)."""
+    _, cap, stride = offsets(bound)
+    sk = int(cap[:k].sum())
+    l = np.asarray(limbs, dtype=np.uint64).reshape(n, stride)[:, :sk].reshape(-1).copy()
+    d = np.asarray(deg, dtype=np.uint32).reshape(n, len(bound))[:, :k].reshape(-1).copy()
+    return l, d, np.ascontiguousarray(np.asarray(bound, dtype=np.uint32)[:k])

@@ -311,3 +311,33 @@ def test_bad_input_is_flagged(H):
     ctx.apply2(H.HomomorphicAddition, c, c)
     with pytest.raises(H.EngineError):
         ctx.synchronize()
+
+
+@pytest.mark.parametrize("k,n", [(8, 4), (12, 2)])
+def test_mul_low_parity(H, oracle, k, n):
+    """u32 multiply, low k result bits at the bench parameters: the GPU
+    reads the low k bits of u32 ciphertexts in place; the oracle runs the k-bit circuit on them."""
+    from helpers import low_bits
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 81)
+    sk, pk, _ = keys(*params, 81)
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, np.uint32, n, 82)
+    cp = ctx.mul_low(ca, cb, k)
+    dec_bytes = ctx.decrypt_bytes(cp).cpu().numpy() if k % 8 == 0 else None
+    ctx.synchronize()
+    bound = fresh_bound(128, 128, 32)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    lak, dak, bk = low_bits(la, da, bound, n, k)
+    lbk, dbk, _ = low_bits(lb, db, bound, n, k)
+    ob = H.mul_out_bounds(bk, bk)
+    assert np.array_equal(cp.bound, ob)
+    rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, n, ob)
+    gl, gd = cp.to_host()
+    assert_batches_equal(gl, gd, rl, rd, ob, n, f"mul low {k}")
+    if dec_bytes is not None:
+        rdec = oracle.decrypt_batch(sk, rl, rd, ob, k, n).reshape(n, -1)
+        assert np.array_equal(dec_bytes, rdec)
+        want = ((a.astype(np.uint64) * b) & ((1 << k) - 1)).astype(np.uint64)
+        got = dec_bytes.astype(np.uint64) @ (256 ** np.arange(k // 8, dtype=np.uint64))
+        assert np.array_equal(got, want)

@@ -131,3 +131,28 @@ def test_gates_roundtrip(oracle, op, f):  # uint.rs:108-174 at (32, 8, 8, 8) / (
     lo, do = oracle.gate_batch(op, la, da, bound, lb, db, bound, 8, 2, ob)
     dec = oracle.decrypt_batch(sk, lo, do, ob, 8, 2).reshape(-1)
     assert dec.tolist() == [f(int(x), int(y)) for x, y in zip(a, b)]
+
+
+@pytest.mark.parametrize("signed", [False, True])
+def test_mul_low_bits_identity(oracle, signed):
+    """output bits 0..k-1 of the L-bit carry-save multiplier equal the
+    k-bit unsigned circuit on the low k input bits (common.rs:66-155: column i reads only input
+    bits <= i; the signed flips live in column L-1)."""
+    from helpers import low_bits
+    d, dp, delta, tau = 32, 8, 1, 8
+    sk, pk, _ = keys(d, dp, delta, tau, 71)
+    n, L, k = 2, 16, 8
+    bound = fresh_bound(d, dp, L)
+    a, b = plain(n, np.uint16, 1), plain(n, np.uint16, 2)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), masks(n, L, tau, 3), bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), masks(n, L, tau, 4), bound)
+    from homomorph import mul_out_bounds
+    ob = mul_out_bounds(bound, bound, signed)
+    lo, do = oracle.mul_batch(la, da, bound, lb, db, bound, L, n, ob, signed=signed)
+    la8, da8, b8 = low_bits(la, da, bound, n, k)
+    lb8, db8, _ = low_bits(lb, db, bound, n, k)
+    ob8 = mul_out_bounds(b8, b8)
+    assert np.array_equal(ob8, ob[:k])
+    l8, d8 = oracle.mul_batch(la8, da8, b8, lb8, db8, b8, k, n, ob8)
+    got_l, got_d, _ = low_bits(lo, do, ob, n, k)
+    assert np.array_equal(got_d, d8) and np.array_equal(got_l, l8)
