@@ -44,8 +44,15 @@ def setup_dist(gpus):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU; HM_BENCH_BACKEND=gloo with more ranks than GPUs is a rehearsal mode
+        # for a one-GPU box (ranks share the card), never the measured configuration
+        backend = os.environ.get("HM_BENCH_BACKEND", "nccl")
+        dev = local % torch.cuda.device_count() if backend == "gloo" else local
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
