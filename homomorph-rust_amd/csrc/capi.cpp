@@ -543,6 +543,11 @@ hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) {
     D.out = out;
     D.status = c->d_status;
     fill_bounds(D.ib, in);
+    for (uint32_t i = 0, o = 0; i < in->nbits; ++i) {
+        D.ioff.b[i] = o;
+        o += cap_of(in->bound[i]);
+        D.maxcap = std::max(D.maxcap, cap_of(in->bound[i]));
+    }
     DeviceGuard g(c->device);
     return launch_decrypt(D, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }

@@ -66,6 +66,8 @@ struct DecArgs {
     uint8_t *out;
     int *status;
     Bounds ib;
+    Bounds ioff;     // limb offset of each bit within a value (prefix sums of the caps)
+    uint32_t maxcap; // widest bit (limbs): picks lane-per-bit or wave-per-value
 };
 
 // Gates and the carry-save multiplier keep their intermediates in a per-value global workspace.

@@ -775,8 +775,9 @@ int launch_encrypt(const EncArgs &E, void *stream) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Decryption: bit = parity(C & z) with z_k = (X^k mod S)(0).  One wavefront per value; lanes
-// stride over the value's limbs (coalesced), accumulate per-bit parities, XOR-reduce.
+// Decryption: bit = parity(C & z) with z_k = (X^k mod S)(0).  Wide ciphertexts (circuit outputs):
+// one wavefront per value; lanes stride over the value's limbs (coalesced), accumulate per-bit
+// parities, XOR-reduce.
 __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
     const int wave = (int)rfl(threadIdx.x >> 6);
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -814,8 +815,44 @@ __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
     }
 }
 
+// Narrow ciphertexts (fresh ones: 5 limbs at d+dp = 256): one lane per ciphertext bit.  A lane
+// XORs (limb & z) over its bit's limbs and takes one popcount parity; the wave's 64 parities are
+// 64 consecutive plaintext bits (bit g of the flattened stream = byte g/8, bit g%8, because
+// nbits = 8 nbytes), so one ballot gives 8 output bytes.  Lanes read consecutive polynomials:
+// the loads stream the batch once.
+__global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t total = D.n * D.nbits;
+    uint32_t p = 0;
+    if (g < total) {
+        const uint64_t e = g / D.nbits;
+        const uint32_t k = (uint32_t)(g % D.nbits);
+        const uint64_t *src = D.in.limbs + e * D.in.stride + D.ioff.b[k];
+        const uint32_t cap = cap_of(D.ib.b[k]); // <= zlimbs (the host sizes z for the widest bit)
+        uint64_t acc = 0;
+        for (uint32_t l = 0; l < cap; ++l) acc ^= src[l] & D.z[l];
+        p = (uint32_t)__builtin_popcountll(acc) & 1u;
+    }
+    const uint64_t bits = __ballot(p);
+    const uint64_t g0 = g - (uint64_t)lane_id();
+    if (lane_id() == 0 && g0 < total) {
+        uint8_t *dst = D.out + g0 / 8;
+        if (g0 + 64 <= total && ((uintptr_t)dst & 7u) == 0) {
+            *(uint64_t *)dst = bits;
+        } else {
+            for (uint64_t b = 0; b < 8 && g0 + 8 * b < total; ++b) dst[b] = (uint8_t)(bits >> (8 * b));
+        }
+    }
+}
+
 int launch_decrypt(const DecArgs &D, void *stream) {
     if (D.n == 0) return 0;
+    if (D.maxcap <= 32 && !getenv("HM_DEC_WAVE")) {
+        const uint64_t blocks = (D.n * D.nbits + 255) / 256;
+        hipLaunchKernelGGL(decrypt_bits_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                           (hipStream_t)stream, D);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     const char *env = getenv("HM_DEC_WPB");
     const uint32_t wpb = env ? (uint32_t)atoi(env) : 4u;
     const uint64_t blocks = (D.n + wpb - 1) / wpb;
