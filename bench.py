@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """Headline benchmark: homomorphic u32 additions per second at d = d' = tau = 128, delta = 1.
 
-One step = one batched launch of the fused ripple-carry adder (src/impls/numbers/common.rs:37-56)
-over `--batch` u32 ciphertext pairs per GPU (BASELINE.json configs[1]: batch 4096), inputs
-already resident in HBM.  Multi-GPU: one process per GPU (torchrun), each rank adds its own
-shard (weak scaling, no data-path collective); keys are broadcast once over RCCL at setup and the
-decrypt-check digests are reduced after the timed region.
+One step = one batched launch of the ripple-carry adder (src/impls/numbers/common.rs:37-56) over
+`--batch` u32 ciphertext pairs per GPU (BASELINE.json configs[1]: batch 4096), inputs already
+resident in HBM.  Multi-GPU: one process per GPU (torchrun), each rank adds its own shard (weak
+scaling, no data-path collective); keys are broadcast once over RCCL at setup, and after the timed
+region the decrypted results are gathered over RCCL (all_gather) and checked on rank 0.
+
+`--workload mixed` runs configs[4] instead: one u32 add plus one u32 multiply (low 8 result bits)
+per value at d = dp = tau = 256, global batch 2^20 split over the ranks (strong scaling).
 
 Prints ONE JSON line (rank 0).  Besides the contract fields it carries
   roofline      HBM roofline of the add kernel: algorithmic bytes per launch / kernel time
@@ -80,9 +83,9 @@ def broadcast_keys(world, rank, device, sk=None, pk=None, params=PARAMS):
     return skt.cpu().numpy().view(np.uint64), pkt.cpu().numpy().view(np.uint64)
 
 
-def make_context(world, rank, device):
+def make_context(world, rank, device, params=PARAMS):
     """Keys are generated on rank 0 and broadcast to every rank (setup, untimed)."""
-    ctx = H.Context(H.Parameters(*PARAMS), device=device)
+    ctx = H.Context(H.Parameters(*params), device=device)
     sk = pk = None
     if rank == 0:
         ctx.seed_rng(0xB0B)
@@ -90,7 +93,7 @@ def make_context(world, rank, device):
         ctx.generate_public_key()
         sk, pk = ctx.get_secret_key().limbs, ctx.get_public_key().limbs
     if world > 1:
-        sk, pk = broadcast_keys(world, rank, device, sk, pk)
+        sk, pk = broadcast_keys(world, rank, device, sk, pk, params)
         if rank != 0:
             ctx.set_secret_key(H.SecretKey(sk))
             ctx.set_public_key(H.PublicKey(pk))
@@ -106,14 +109,18 @@ def shard_inputs(rank, n):
     return a, b
 
 
-def reduce_over_ranks(world, device, correct, wall):
-    """(sum of correct results, max wall time) over ranks; identity at world 1."""
-    c = torch.tensor([int(correct)], dtype=torch.int64, device=device)
+def gather_results(world, device, res, wall):
+    """The final result gather (RCCL all_gather on GPUs, gloo in the CPU tests): every rank's
+    decrypted plaintext bytes (n x k uint8, equal n per rank) and wall time reach every rank.
+    Returns (world*n x k numpy array in rank order, max wall time).  Identity at world 1."""
+    if world == 1:
+        return res.cpu().numpy(), float(wall)
+    parts = [torch.empty_like(res) for _ in range(world)]
+    dist.all_gather(parts, res.contiguous())
     w = torch.tensor([float(wall)], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-    return int(c.item()), float(w.item())
+    walls = [torch.empty_like(w) for _ in range(world)]
+    dist.all_gather(walls, w)
+    return torch.cat(parts).cpu().numpy(), max(float(x.item()) for x in walls)
 
 
 def time_loop(fn, steps, warmup, world, stream=None):
@@ -218,24 +225,15 @@ def secondary_metrics(ctx, device, steps):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="u32 pairs per GPU (configs[1])")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "add_traffic.json"),
-                    help="PMC-derived HBM bytes per add launch (written by profiles/pmc.py)")
-    args = ap.parse_args()
+MIXED_PARAMS = (256, 256, 1, 256)  # BASELINE.json configs[4]: d = dp = tau = 256, delta = 1
+MIXED_CHUNK = 131072                # values per launch (the 8-GPU shard of 2^20)
+MUL_LOW_K = 8                       # result bits of the multiply half
 
-    world, rank, local = setup_dist(args.gpus)
-    device = torch.device("cuda", torch.cuda.current_device())
+
+def run_add(args, world, rank, device):
+    """configs[1]: u32 homomorphic add, batch 4096 per GPU (weak scaling)."""
     ctx = make_context(world, rank, device)
-
-    n = args.batch
+    n = args.batch or 4096
     a, b = shard_inputs(rank, n)
     gen = torch.Generator(device=device)
     gen.manual_seed(31 + rank)
@@ -247,9 +245,10 @@ def main():
     wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, args.warmup, world,
                            ctx.stream)
     ctx.synchronize()  # raises on any device-side error flag
-    # verification (untimed): decrypt and compare; digests reduced over RCCL
-    dec = ctx.decrypt(out)
-    correct, wall = reduce_over_ranks(world, device, np.sum(dec == (a + b).astype(np.uint32)), wall)
+    # verification (untimed): decrypt on device, gather the plaintexts over RCCL, check on rank 0
+    got, wall = gather_results(world, device, ctx.decrypt_bytes(out), wall)
+    want = np.concatenate([sum(shard_inputs(r, n)).astype(np.uint32) for r in range(world)])
+    correct = int(np.sum(got.view("<u4").reshape(-1) == want))
     total = n * world * args.steps
 
     in_bytes = 8 * (ca.stride + cb.stride)
@@ -295,8 +294,93 @@ def main():
         except Exception as e:  # reported, never fatal to the headline line
             result["secondary"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb_ = cpu_baseline_add(args.cpu_seconds)
-        result["cpu_baseline"] = cb_
+        result["cpu_baseline"] = cpu_baseline_add(args.cpu_seconds)
+    return result
+
+
+def run_mixed(args, world, rank, device):
+    """configs[4]: u32 mixed add + mul at d = dp = tau = 256, global batch 2^20 sharded over the
+    ranks (strong scaling), RCCL gather of the decrypted results.  Per value: one u32 add and one
+    u32 multiply reduced to its low MUL_LOW_K result bits (the full u32 multiply circuit is
+    infeasible; its low bits are bit-exact, row A14).  Each rank processes its
+    shard in launches of MIXED_CHUNK values."""
+    ctx = make_context(world, rank, device, MIXED_PARAMS)
+    glob = args.batch or (1 << 20)
+    if glob % world:
+        raise SystemExit("--batch must divide by the number of ranks")
+    n = glob // world
+    a, b = shard_inputs(rank, n)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(31 + rank)
+    ca, cb = ctx.encrypt(a, generator=gen), ctx.encrypt(b, generator=gen)
+    sums = H.Ciphered.empty(n, H.add_out_bounds(ca.bound, cb.bound), device, np.dtype(np.uint32))
+    kb = H.mul_out_bounds(ca.bound[:MUL_LOW_K], cb.bound[:MUL_LOW_K])
+    prods = H.Ciphered.empty(n, kb, device, np.dtype(np.uint8))
+    chunks = [(lo, min(n, lo + MIXED_CHUNK)) for lo in range(0, n, MIXED_CHUNK)]
+    views = [tuple(H.value_slice(c, lo, hi) for c in (ca, cb, sums, prods)) for lo, hi in chunks]
+    ctx.synchronize()
+
+    def step():
+        for va, vb, vs, vp in views:
+            H.add_into(ctx, va, vb, vs)
+            H.mul_low_into(ctx, va, vb, MUL_LOW_K, vp)
+
+    wall, ev_s = time_loop(step, args.steps, args.warmup, world, ctx.stream)
+    ctx.synchronize()
+    res = torch.cat([ctx.decrypt_bytes(sums), ctx.decrypt_bytes(prods)], dim=1)  # n x 5 bytes
+    got, wall = gather_results(world, device, res, wall)
+    want_s, want_p = [], []
+    for r in range(world):
+        ra, rb = shard_inputs(r, n)
+        want_s.append((ra + rb).astype(np.uint32))
+        want_p.append((ra.astype(np.uint64) * rb % (1 << MUL_LOW_K)).astype(np.uint8))
+    ok_s = int(np.sum(np.ascontiguousarray(got[:, :4]).view("<u4").reshape(-1) ==
+                      np.concatenate(want_s)))
+    ok_p = int(np.sum(got[:, 4] == np.concatenate(want_p)))
+    total = glob * args.steps
+    return {
+        "metric": "homomorphic u32 ops/sec (add, mul) at d=dp=tau=256; 1/2/4/8 MI355X",
+        "value": total / wall,
+        "unit": f"u32 values/s (one add + one mul, low {MUL_LOW_K} result bits, per value)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * wall / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: seeded u32 plaintexts, seeded keys, device-drawn subset masks",
+        "config": {"workload": "u32 mixed add+mul (configs[4])", "global_batch": glob,
+                   "batch_per_gpu": n, "launch_chunk": MIXED_CHUNK, "d": MIXED_PARAMS[0],
+                   "dp": MIXED_PARAMS[1], "delta": MIXED_PARAMS[2], "tau": MIXED_PARAMS[3],
+                   "mul_result_bits": MUL_LOW_K, "parallelism": f"batch-sharded x{world}",
+                   "collective": "RCCL all_gather of decrypted results (5 B per value)"},
+        "verified": {"correct_sums": ok_s, "correct_products": ok_p, "of": glob},
+        "kernel_ms_per_step": 1e3 * ev_s / args.steps,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["add", "mixed"], default="add",
+                    help="add: configs[1] (headline); mixed: configs[4]")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="add: u32 pairs per GPU (default 4096); mixed: global batch (2^20)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "add_traffic.json"),
+                    help="PMC-derived HBM bytes per add launch (scripts/traffic_json.py)")
+    args = ap.parse_args()
+
+    world, rank, local = setup_dist(args.gpus)
+    device = torch.device("cuda", torch.cuda.current_device())
+    run = run_add if args.workload == "add" else run_mixed
+    result = run(args, world, rank, device)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

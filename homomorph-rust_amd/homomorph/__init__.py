@@ -566,3 +566,18 @@ def mul_into(ctx: Context, a: Ciphered, b: Ciphered, out: Ciphered, signed=False
     ca, cb, co = a._c(), b._c(), out._c()
     ctx._launch(lambda: lib().hm_mul_batch(ctx._h, ctypes.byref(ca), ctypes.byref(cb),
                                            int(signed), ctypes.byref(co)), "hm_mul_batch")
+
+
+def mul_low_into(ctx: Context, a: Ciphered, b: Ciphered, k: int, out: Ciphered) -> None:
+    """hm_mul_low_batch into a preallocated k-bit output (bounds: mul_out_bounds of the first k
+    input bounds)."""
+    ca, cb, co = a._c(), b._c(), out._c()
+    ctx._launch(lambda: lib().hm_mul_low_batch(ctx._h, ctypes.byref(ca), ctypes.byref(cb), k,
+                                               ctypes.byref(co)), "hm_mul_low_batch")
+
+
+def value_slice(c: Ciphered, lo: int, hi: int) -> Ciphered:
+    """Values [lo, hi) of a batch as a view (one value's limbs and degrees are contiguous)."""
+    s = c.stride
+    return Ciphered(c.limbs[lo * s: hi * s], c.degree[lo:hi], c.bound, c.nbits, hi - lo,
+                    c.plain_dtype)

@@ -38,14 +38,20 @@ def _worker(rank, world, port, q):
         if rank == 0:
             sk, pk, _ = oracle.keygen(*bench.PARAMS, 0xB0B)
         sk, pk = bench.broadcast_keys(world, rank, dev, sk, pk)
+        # the mixed workload's d = dp = tau = 256 keys travel the same way
+        sk2 = pk2 = None
+        if rank == 0:
+            sk2, pk2, _ = oracle.keygen(*bench.MIXED_PARAMS, 0xB0C)
+        sk2, pk2 = bench.broadcast_keys(world, rank, dev, sk2, pk2, bench.MIXED_PARAMS)
         a, b = bench.shard_inputs(rank, 64)
-        correct, wall = bench.reduce_over_ranks(world, dev, 60 + rank, 1.5 + rank)
-        q.put((rank, sk.copy(), pk.copy(), a.copy(), correct, wall))
+        res = torch.from_numpy((a + b).astype(np.uint32).view(np.uint8).reshape(-1, 4).copy())
+        got, wall = bench.gather_results(world, dev, res, 1.5 + rank)
+        q.put((rank, sk.copy(), pk.copy(), a.copy(), got.copy(), wall, pk2.copy()))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_keys_shards_and_reduction():
+def test_two_rank_keys_shards_and_gather():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -56,8 +62,8 @@ def test_two_rank_keys_shards_and_reduction():
         p.start()
     res = {}
     for _ in range(world):
-        r, sk, pk, a, correct, wall = q.get(timeout=240)
-        res[r] = (sk, pk, a, correct, wall)
+        r, sk, pk, a, got, wall, pk2 = q.get(timeout=240)
+        res[r] = (sk, pk, a, got, wall, pk2)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -65,11 +71,14 @@ def test_two_rank_keys_shards_and_reduction():
     from oracle import oracle_py as oracle
     import bench
     sk0, pk0, _ = oracle.keygen(*bench.PARAMS, 0xB0B)
+    _, pk20, _ = oracle.keygen(*bench.MIXED_PARAMS, 0xB0C)
+    want = np.concatenate([sum(bench.shard_inputs(r, 64)).astype(np.uint32) for r in range(world)])
     for r in range(world):
-        sk, pk, a, correct, wall = res[r]
+        sk, pk, a, got, wall, pk2 = res[r]
+        assert np.array_equal(pk2[:, : pk20.shape[1]], pk20)
         assert np.array_equal(sk[: len(sk0)], sk0) and not sk[len(sk0):].any()
         assert np.array_equal(pk[:, : pk0.shape[1]], pk0)
-        assert correct == 60 + 61          # summed over ranks
+        assert np.array_equal(got.view("<u4").reshape(-1), want)  # every rank's results, rank order
         assert wall == 2.5                 # max over ranks
     assert not np.array_equal(res[0][2], res[1][2])  # distinct shards
 
