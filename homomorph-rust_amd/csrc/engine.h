@@ -40,6 +40,7 @@ struct AddArgs {
     uint32_t cw;                      // chain: carry buffer words
     uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
     uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)
+    uint32_t fused;                   // one kernel: products computed into the staged LDS layout
     uint32_t debug_skip;              // timing experiments only (HM_DEBUG_SKIP): 1 prep, 2 chain product
     int *status;
     Bounds ab, bb, ob;

@@ -238,6 +238,53 @@ __device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
     return o;
 }
 
+// Stage bits [i0, i0+nb) of one value's input (u64 limbs, exact degrees) into LDS words: bit
+// i0+t at dst + t*cnt, its word count at nw[t] (0 = null).  Lanes stride over the range's
+// contiguous limbs (all its bits at once, coalesced); every limb is validated against its bit's
+// degree word as in load_bit.  src/deg point at the value's first limb / degree word.
+__device__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
+                           const Bounds &B, uint32_t i0, uint32_t nb, uint32_t *dst, uint32_t cnt,
+                           uint32_t *nw, int *status) {
+    const int lane = lane_id();
+    src += limb_off(B, i0);
+    deg += i0;
+    uint32_t total = 0;
+    for (uint32_t t = 0; t < nb; ++t) total += cap_of(B.b[i0 + t]);
+    uint32_t t = 0, lo = 0, hi = nb ? cap_of(B.b[i0]) : 0;
+    bool bad = false;
+    for (uint32_t g = lane; g < total; g += kWave) {
+        while (g >= hi) ++t, lo = hi, hi += cap_of(B.b[i0 + t]);
+        const uint32_t d = deg[t], k = g - lo;
+        uint64_t v = src[g];
+        if (d > B.b[i0 + t]) {
+            bad = true;
+            continue;
+        }
+        const uint32_t nl = d / 64 + 1;
+        if (k >= nl) {
+            bad |= v != 0; // limbs above the degree must be zero (layout invariant)
+            continue;
+        }
+        if (k == nl - 1) {
+            const uint32_t tb = d % 64;
+            const uint64_t keep = (~0ull) >> (63 - tb);
+            bad |= (v & ~keep) != 0;
+            v &= keep;
+            if (d > 0 && !((v >> tb) & 1ull)) bad = true;
+        }
+        dst[t * cnt + 2 * k] = (uint32_t)v;
+        dst[t * cnt + 2 * k + 1] = (uint32_t)(v >> 32);
+    }
+    if (__any(bad) && lane == 0) flag(status, HM_ERR_BAD_INPUT);
+    wsync();
+    for (uint32_t k = lane; k < nb; k += kWave) {
+        const uint32_t d = deg[k];
+        uint32_t n = d / 32 + 1;
+        if (d > B.b[i0 + k] || (d == 0 && !(dst[k * cnt] & 1u))) n = 0;
+        nw[k] = n;
+    }
+}
+
 __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
     const uint32_t wave = rfl(threadIdx.x >> 6);
@@ -247,7 +294,8 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     if (e >= A.n) return;
     const int lane = lane_id();
     const uint32_t L = A.nbits;
-    const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits part, part+wpv, ...
+    const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits [i0, i0 + nmine)
+    const uint32_t i0 = min(L, part * bpw), nmine = min(L, i0 + bpw) - i0;
     // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][P: bpw cntP][na nb dAB dP]
     uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
     uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
@@ -260,23 +308,16 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
 
     // stage + validate this wave's bits (every bit is validated, the last one too)
-    uint32_t nmine = 0;
-    for (uint32_t i = part; i < L; i += A.wpv, ++nmine) {
-        const int na = load_bit(pa + limb_off(A.ab, i), rfl(da[i]), A.ab.b[i], Al + nmine * A.cntA,
-                                A.status);
-        const int nb = load_bit(pb + limb_off(A.bb, i), rfl(db[i]), A.bb.b[i], Bl + nmine * A.cntB,
-                                A.status);
-        if (lane == 0) nAl[nmine] = (uint32_t)na, nBl[nmine] = (uint32_t)nb;
-    }
+    stage_bits(pa, da, A.ab, i0, nmine, Al, A.cntA, nAl, A.status);
+    stage_bits(pb, db, A.bb, i0, nmine, Bl, A.cntB, nBl, A.status);
     for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
     // products only for bits < L-1 (the last bit has no outgoing carry)
-    const uint32_t nprod = (A.debug_skip & 1u) ? 0u
-                           : (part < L - 1 ? (L - 2 - part) / A.wpv + 1 : 0u);
+    const uint32_t nprod = (A.debug_skip & 1u) ? 0u : min(nmine, (L - 1) - min(i0, L - 1));
 
     // x_i = a_i ^ b_i for every bit: LDS for the P products, workspace for the chain's sum bits
     for (uint32_t f = lane; f < nmine * A.cntX; f += kWave) {
-        const uint32_t t = f / A.cntX, m = f % A.cntX, i = part + t * A.wpv;
+        const uint32_t t = f / A.cntX, m = f % A.cntX, i = i0 + t;
         const int na = (int)nAl[t], nb = (int)nBl[t];
         const uint32_t x = ((int)m < na ? Al[t * A.cntA + m] : 0u) ^
                            ((int)m < nb ? Bl[t * A.cntB + m] : 0u);
@@ -308,7 +349,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
         const uint32_t t = f / A.cntAB, m = f % A.cntAB;
         const uint32_t w = ABl[f];
-        ABg[(size_t)(part + t * A.wpv) * A.cntAB + m] = w;
+        ABg[(size_t)(i0 + t) * A.cntAB + m] = w;
         if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
     }
     wsync();
@@ -323,12 +364,12 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) {
         const uint32_t t = f / A.cntP, m = f % A.cntP;
         const uint32_t w = Pl[f] ^ (m < A.cntX ? Xl[t * A.cntX + m] : 0u);
-        Pg[(size_t)(part + t * A.wpv) * A.cntP + m] = w;
+        Pg[(size_t)(i0 + t) * A.cntP + m] = w;
         if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
     }
     wsync();
     for (uint32_t t = lane; t < nprod; t += kWave) {
-        const uint32_t i = part + t * A.wpv;
+        const uint32_t i = i0 + t;
         degABg[i] = dAB[t];
         degPg[i] = dP[t];
     }
@@ -477,8 +518,116 @@ __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
     }
 }
 
+// One kernel per add batch: each wavefront computes its value's carry-independent products
+// (x_i, ab_i, P_i, as add_prep_kernel does with several waves) straight into the staged LDS
+// layout, then runs the staged carry chain.  No workspace round trip through HBM and one launch;
+// the products' VALU work fills issue slots the chain's scalar branches leave idle on the SIMD.
+// The inputs are staged in the (not yet used) carry buffer, so LDS per wave equals the staged
+// chain's.
+template <int WMAX>
+__global__ void __launch_bounds__(256) add_fused_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    const uint32_t L = A.nbits;
+    // LDS: [halo][C: cw][P: (L-1) cntP][AB: (L-1) cntAB][X: L cntX][degP+1: L][degAB+1: L]
+    uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
+    uint32_t *C = Ls + kHalo;
+    uint32_t *Pl = C + A.cw, *ABl = Pl + (size_t)(L - 1) * A.cntP;
+    uint32_t *Xl = ABl + (size_t)(L - 1) * A.cntAB, *dPl = Xl + (size_t)L * A.cntX, *dABl = dPl + L;
+    // inputs inside the carry buffer: [a: L cntA][b: L cntB][na: L][nb: L]
+    uint32_t *Al = C, *Bl = Al + (size_t)L * A.cntA, *nAl = Bl + (size_t)L * A.cntB, *nBl = nAl + L;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    uint32_t *dout = A.out.degree + e * L;
+
+    stage_bits(A.a.limbs + e * A.a.stride, A.a.degree + e * L, A.ab, 0, L, Al, A.cntA, nAl, A.status);
+    stage_bits(A.b.limbs + e * A.b.stride, A.b.degree + e * L, A.bb, 0, L, Bl, A.cntB, nBl, A.status);
+    const uint32_t nprod = L - 1; // the last bit has no outgoing carry
+    for (uint32_t k = lane; k < 2 * L; k += kWave) dPl[k] = 0u; // dPl, dABl
+    for (uint32_t k = lane; k < nprod * A.cntAB; k += kWave) ABl[k] = 0u;
+    for (uint32_t k = lane; k < nprod * A.cntP; k += kWave) Pl[k] = 0u;
+    wsync();
+    // x_i = a_i ^ b_i, every bit
+    for (uint32_t f = lane; f < L * A.cntX; f += kWave) {
+        const uint32_t t = f / A.cntX, m = f % A.cntX;
+        const int na = (int)nAl[t], nb = (int)nBl[t];
+        Xl[f] = ((int)m < na ? Al[t * A.cntA + m] : 0u) ^ ((int)m < nb ? Bl[t * A.cntB + m] : 0u);
+    }
+    // products by rows, lanes over (bit t, multiplier word q); rows meet in LDS through ds_xor
+    const uint32_t cq = A.cntX;
+    auto for_rows = [&](auto &&row) {
+        const uint32_t dt = kWave / cq, dq = kWave % cq;
+        uint32_t t = (uint32_t)lane / cq, q = (uint32_t)lane % cq;
+        for (uint32_t f0 = 0; f0 < nprod * cq; f0 += kWave) {
+            if (t < nprod) row(t, q);
+            t += dt, q += dq;
+            if (q >= cq) q -= cq, ++t;
+        }
+    };
+    wsync();
+    for_rows([&](uint32_t t, uint32_t q) { // ab_i = a_i * b_i
+        if ((int)q < (int)nAl[t])
+            clmul_row_xor(Al[t * A.cntA + q], Bl + t * A.cntB, (int)nBl[t], ABl + t * A.cntAB + q);
+    });
+    wsync();
+    for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
+        const uint32_t w = ABl[f];
+        if (w) atomicMax(&dABl[f / A.cntAB], (f % A.cntAB) * 32 + 32 - __builtin_clz(w));
+    }
+    wsync();
+    for_rows([&](uint32_t t, uint32_t q) { // x_i * ab_i
+        const int nx = max((int)nAl[t], (int)nBl[t]);
+        if ((int)q < nx)
+            clmul_row_xor(Xl[t * A.cntX + q], ABl + t * A.cntAB, bitwords((int)dABl[t]),
+                          Pl + t * A.cntP + q);
+    });
+    wsync();
+    for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) { // P_i = x_i ^ x_i * ab_i
+        const uint32_t t = f / A.cntP, m = f % A.cntP;
+        const uint32_t w = Pl[f] ^ (m < A.cntX ? Xl[t * A.cntX + m] : 0u);
+        Pl[f] = w;
+        if (w) atomicMax(&dPl[t], m * 32 + 32 - __builtin_clz(w));
+    }
+    // the inputs are consumed: clear the carry buffer and its halo
+    for (uint32_t k = lane; k < kHalo + A.cw; k += kWave) Ls[k] = 0u;
+    wsync();
+
+    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    uint32_t offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        store_sum_x(Xl + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
+                    A.status);
+        if (i + 1 < L) {
+            const int np = bitwords((int)rfl(dPl[i])), nab = bitwords((int)rfl(dABl[i]));
+            int nout;
+            wsync(); // the sum bit's reads of C precede the in-place product's writes
+            nc = words_of(wave_mul<kQBig, WMAX, true>(Pl + (size_t)i * A.cntP, np, C, nc,
+                                                      ABl + (size_t)i * A.cntAB, nab, C, &nout));
+            wsync();
+        }
+        offo += cap_of(A.ob.b[i]);
+    }
+}
+
 int launch_add(const AddArgs &a, void *stream) {
     if (a.n == 0) return 0;
+    if (a.fused) {
+        const uint64_t blocks = (a.n + kAddWavesPerBlock - 1) / kAddWavesPerBlock;
+        const size_t lds = (size_t)a.chain_lds * 4 * kAddWavesPerBlock;
+        const uint32_t need = (a.max_prod_words + 63) / 64;
+#define HM_LAUNCH_FUSED(WM)                                                                       \
+    hipLaunchKernelGGL((add_fused_kernel<WM>), dim3((unsigned)blocks), dim3(64 * kAddWavesPerBlock), \
+                       lds, (hipStream_t)stream, a)
+        if (need <= 4) HM_LAUNCH_FUSED(4);
+        else if (need <= 8) HM_LAUNCH_FUSED(8);
+        else if (need <= 12) HM_LAUNCH_FUSED(12);
+        else if (need <= 16) HM_LAUNCH_FUSED(16);
+        else HM_LAUNCH_FUSED(24);
+#undef HM_LAUNCH_FUSED
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     // prep: wpv waves per value, 4 waves per block
     {
         const uint64_t waves = a.n * a.wpv;

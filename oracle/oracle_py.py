@@ -2,7 +2,7 @@
 
 Loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; never by the product.
 All arrays are numpy; the batch layout is the one documented in oracle/homomorph_oracle.h and
-shared with the GPU engine (homomorph-rust_amd/csrc/layout.h).
+shared with the GPU engine (include/homomorph_gpu.h, "Batch layout").
 """
 from __future__ import annotations
 

@@ -1,0 +1,172 @@
+"""GPU parity at BASELINE.json's full sizes, through sampled oracle checks and size-independent
+properties (the oracle alone would take minutes to hours on the whole batches).
+
+  configs[1] u32 add, batch 4096, d=dp=tau=128       sampled values bit-exact vs the oracle;
+                                                      s_0 = a_0 ^ b_0 (bit 0 has no carry);
+                                                      idempotent re-run; degrees within bounds;
+                                                      plaintext sums (up to the scheme's noise)
+  configs[2] u32 enc+dec, batch 65536                 decrypt(encrypt(x)) = x for every value;
+                                                      linearity E(x;m) ^ E(y;m) = x ^ y;
+                                                      sampled values bit-exact vs the oracle
+  configs[3] u32 mul (low 12 bits), batch 1024        every value's low 12 product bits decrypt
+                                                      (up to noise); one value bit-exact
+  configs[4] mixed add + mul-low-8, d=dp=tau=256,     one launch chunk (131072 values, the 8-GPU
+             the per-GPU shard                        shard of 2^20): every value decrypts; two
+                                                      sampled values bit-exact vs the oracle
+"""
+import numpy as np
+import pytest
+
+from helpers import (as_bytes, assert_batches_equal, fresh_bound, keys, low_bits, masks, offsets,
+                     plain)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import homomorph
+    homomorph.lib()  # loud failure if the engine is not built
+    return homomorph
+
+
+def make_ctx(H, params, seed):
+    ctx = H.Context(H.Parameters(*params))
+    ctx.seed_rng(seed)
+    ctx.generate_secret_key()
+    ctx.generate_public_key()
+    return ctx
+
+
+def _rows(H, c, idx):
+    """Values idx of a device batch, copied to the host as one batch (limbs, degrees)."""
+    parts = [H.value_slice(c, int(i), int(i) + 1).to_host() for i in idx]
+    return (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+
+
+def test_add_config1_full_batch(H, oracle):
+    params, n = (128, 128, 1, 128), 4096
+    ctx = make_ctx(H, params, 11)
+    sk, pk, _ = keys(*params, 11)
+    a, b = plain(n, np.uint32, 12), plain(n, np.uint32, 13)
+    ma, mb = masks(n, 32, 128, 14), masks(n, 32, 128, 15)
+    ca, cb = ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb)
+    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    dec = ctx.decrypt(cs)
+    ctx.synchronize()
+    gl, gd = cs.to_host()
+    ob = cs.bound
+    # idempotent: a second launch over the same inputs writes the same bits
+    H.add_into(ctx, ca, cb, cs)
+    ctx.synchronize()
+    gl2, gd2 = cs.to_host()
+    assert np.array_equal(gl, gl2) and np.array_equal(gd, gd2)
+    # degrees within the static bounds; bit 0 = a_0 ^ b_0 exactly (no incoming carry)
+    assert (gd.reshape(n, 32) <= ob[None, :]).all()
+    al, _ = ca.to_host()
+    bl, _ = cb.to_host()
+    _, capa, sa = offsets(ca.bound)
+    _, capo, so = offsets(ob)
+    s0 = gl.reshape(n, so)[:, : capo[0]]
+    x0 = al.reshape(n, sa)[:, : capa[0]] ^ bl.reshape(n, sa)[:, : capa[0]]
+    assert np.array_equal(s0[:, : capa[0]], x0) and not s0[:, capa[0]:].any()
+    # sampled values bit-exact vs the oracle
+    idx = np.sort(np.random.default_rng(16).choice(n, 8, replace=False))
+    bound = fresh_bound(128, 128, 32)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a[idx]), ma[idx], bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b[idx]), mb[idx], bound)
+    rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, 32, len(idx), ob)
+    sl, sd = _rows(H, cs, idx)
+    assert_batches_equal(sl, sd, rl, rd, ob, len(idx), "config1 sampled")
+    rdec = oracle.decrypt_batch(sk, rl, rd, ob, 32, len(idx)).view(np.uint32).reshape(-1)
+    assert np.array_equal(dec[idx], rdec)
+    # the scheme's own noise flips a handful of sums at these parameters (2 of 4096 in the bench)
+    assert np.mean(dec == (a + b).astype(np.uint32)) > 0.99
+
+
+def test_encdec_config2_full_batch(H, oracle):
+    import torch
+    params, n = (128, 128, 1, 128), 65536
+    ctx = make_ctx(H, params, 21)
+    sk, pk, _ = keys(*params, 21)
+    x, y = plain(n, np.uint32, 22), plain(n, np.uint32, 23)
+    m = masks(n, 32, 128, 24)
+    cx, cy = ctx.encrypt(x, masks=m), ctx.encrypt(y, masks=m)
+    assert np.array_equal(ctx.decrypt(cx), x)
+    # linearity: same masks -> the public-key sums cancel, leaving the constant x_k ^ y_k per bit
+    d = (cx.limbs ^ cy.limbs).cpu().numpy().view(np.uint64)
+    off, _, stride = offsets(cx.bound)
+    d = d.reshape(n, stride).copy()
+    bits = ((x ^ y)[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1
+    assert np.array_equal(d[:, off], bits.astype(np.uint64))
+    d[:, off] = 0
+    assert not d.any()
+    # sampled values bit-exact vs the oracle
+    ctx.synchronize()
+    idx = np.sort(np.random.default_rng(25).choice(n, 16, replace=False))
+    bound = fresh_bound(128, 128, 32)
+    rl, rd = oracle.encrypt_batch(pk, as_bytes(x[idx]), m[idx], bound)
+    sl, sd = _rows(H, cx, idx)
+    assert_batches_equal(sl, sd, rl, rd, bound, len(idx), "config2 sampled")
+    del cx, cy
+    torch.cuda.empty_cache()
+
+
+def test_mul_low12_config3_full_batch(H, oracle):
+    params, n, k = (128, 128, 1, 128), 1024, 12
+    ctx = make_ctx(H, params, 31)
+    sk, pk, _ = keys(*params, 31)
+    a, b = plain(n, np.uint32, 32), plain(n, np.uint32, 33)
+    ma, mb = masks(n, 32, 128, 34), masks(n, 32, 128, 35)
+    cp = ctx.mul_low(ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb), k)
+    ctx.synchronize()
+    gl, gd = cp.to_host()
+    # decrypt the 12-bit result through a 16-bit view whose top 4 bits are null polynomials
+    ob = cp.bound
+    bound16 = np.concatenate([ob, np.zeros(4, dtype=np.uint32)])
+    _, _, s12 = offsets(ob)
+    l16 = np.concatenate([gl.reshape(n, s12), np.zeros((n, 4), np.uint64)], axis=1).reshape(-1)
+    d16 = np.concatenate([gd.reshape(n, k), np.zeros((n, 4), np.uint32)], axis=1).reshape(-1)
+    c16 = H.Ciphered.from_host(l16, d16, bound16, n, ctx.device, np.dtype(np.uint16))
+    dec = ctx.decrypt(c16)
+    want = ((a.astype(np.uint64) * b) & ((1 << k) - 1)).astype(np.uint16)
+    assert np.mean(dec == want) > 0.99
+    # one value bit-exact vs the oracle (the k-bit circuit on the low k input bits)
+    i = 7
+    bound = fresh_bound(128, 128, 32)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a[i:i + 1]), ma[i:i + 1], bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b[i:i + 1]), mb[i:i + 1], bound)
+    lak, dak, bk = low_bits(la, da, bound, 1, k)
+    lbk, dbk, _ = low_bits(lb, db, bound, 1, k)
+    rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, 1, ob)
+    sl, sd = _rows(H, cp, [i])
+    assert_batches_equal(sl, sd, rl, rd, ob, 1, "config3 sampled")
+
+
+def test_mixed_config4_shard(H, oracle):
+    import torch
+    params, n, k = (256, 256, 1, 256), 131072, 8
+    ctx = make_ctx(H, params, 41)
+    a, b = plain(n, np.uint32, 42), plain(n, np.uint32, 43)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)  # device-drawn masks
+    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    cp = ctx.mul_low(ca, cb, k)
+    assert np.array_equal(ctx.decrypt(cs), (a + b).astype(np.uint32))
+    assert np.array_equal(ctx.decrypt(cp, np.uint8), (a.astype(np.uint64) * b % 256).astype(np.uint8))
+    ctx.synchronize()
+    # two sampled values bit-exact vs the oracle, from the device's own input ciphertexts
+    idx = [5, n - 3]
+    la, da = _rows(H, ca, idx)
+    lb, db = _rows(H, cb, idx)
+    rl, rd = oracle.add_batch(la, da, ca.bound, lb, db, cb.bound, 32, 2, cs.bound)
+    sl, sd = _rows(H, cs, idx)
+    assert_batches_equal(sl, sd, rl, rd, cs.bound, 2, "config4 add sampled")
+    lak, dak, bk = low_bits(la, da, ca.bound, 2, k)
+    lbk, dbk, _ = low_bits(lb, db, cb.bound, 2, k)
+    rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, 2, cp.bound)
+    sl, sd = _rows(H, cp, idx)
+    assert_batches_equal(sl, sd, rl, rd, cp.bound, 2, "config4 mul sampled")
+    del ca, cb, cs, cp
+    torch.cuda.empty_cache()
