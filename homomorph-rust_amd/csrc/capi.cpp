@@ -33,6 +33,7 @@ struct hm_ctx {
     uint32_t pk_maxdeg = 0;
     // device state
     uint64_t *d_pk = nullptr;
+    uint64_t *d_pk_tab = nullptr;      // encryption nibble table (upload_pk), or null
     uint64_t *d_z = nullptr;           // decrypt parity table z_k = (X^k mod S)(0)
     uint32_t z_limbs = 0;
     uint64_t *d_s = nullptr;           // divisor scratch for hm_poly_rem_batch
@@ -42,6 +43,7 @@ struct hm_ctx {
     uint32_t *d_ws_add = nullptr;      // adder workspace (validated inputs, per-bit a_i*b_i)
     size_t ws_add_bytes = 0;
     int *d_status = nullptr;
+    uint32_t cus = 256;                // compute units of the device (grid sizing)
     hipError_t last_hip = hipSuccess;
 };
 
@@ -148,11 +150,32 @@ bool covers(const hm_batch *out, const std::vector<uint32_t> &need) {
     return true;
 }
 
+// Uploads the public key rows, and (when it fits an LDS budget) the encryption nibble table:
+// for every group g of four rows, the 16 XOR combinations T[g][n] = XOR_{k: bit k of n} T_{4g+k}
+// (rows past tau are zero).  Built once per key, so encryption blocks only copy it into LDS.
+// Layout [g][limb pair p][n][2 limbs] (a missing last limb is zero): the 16 entries' copies of
+// one limb pair are 16 B apart, so a wave's per-lane lookups (any n per lane) of one pair are a
+// conflict-free ds_read_b128 -- 16 distinct addresses cover the 64 LDS banks exactly once.
 hm_status upload_pk(hm_ctx *c) {
     DeviceGuard g(c->device);
     if (c->d_pk) (void)hipFree(c->d_pk), c->d_pk = nullptr;
+    if (c->d_pk_tab) (void)hipFree(c->d_pk_tab), c->d_pk_tab = nullptr;
     HM_HIP(c, hipMalloc(&c->d_pk, c->pk.size() * 8));
     HM_HIP(c, hipMemcpy(c->d_pk, c->pk.data(), c->pk.size() * 8, hipMemcpyHostToDevice));
+    const uint32_t G = (c->pk_tau + 3) / 4, PC = c->pk_cap, NP = (PC + 1) / 2;
+    const size_t words = (size_t)G * NP * 16 * 2;
+    if (words * 8 <= kEncTableBytes) {
+        std::vector<uint64_t> tab(words, 0);
+        for (uint32_t grp = 0; grp < G; ++grp)
+            for (uint32_t n = 0; n < 16; ++n)
+                for (uint32_t k = 0; k < 4; ++k)
+                    if (((n >> k) & 1u) && 4 * grp + k < c->pk_tau)
+                        for (uint32_t l = 0; l < PC; ++l)
+                            tab[(((size_t)grp * NP + l / 2) * 16 + n) * 2 + l % 2] ^=
+                                c->pk[(size_t)(4 * grp + k) * PC + l];
+        HM_HIP(c, hipMalloc(&c->d_pk_tab, words * 8));
+        HM_HIP(c, hipMemcpy(c->d_pk_tab, tab.data(), words * 8, hipMemcpyHostToDevice));
+    }
     return HM_OK;
 }
 
@@ -263,6 +286,10 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
         return HM_ERR_HIP;
     }
     c->stream = c->own_stream;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        cus = 256;
+    c->cus = (uint32_t)std::max(cus, 1);
     *out = c;
     return HM_OK;
 }
@@ -273,6 +300,7 @@ void hm_ctx_destroy(hm_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     drop_secret(c);
     if (c->d_pk) (void)hipFree(c->d_pk);
+    if (c->d_pk_tab) (void)hipFree(c->d_pk_tab);
     if (c->d_s) (void)hipFree(c->d_s);
     if (c->d_ws) (void)hipFree(c->d_ws);
     if (c->d_ws_add) (void)hipFree(c->d_ws_add);
@@ -515,11 +543,21 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     if (out->n == 0) return HM_OK;
     EncArgs E{};
     E.pk = c->d_pk, E.tau = c->pk_tau, E.pk_cap = c->pk_cap;
+    E.pk_tab = c->d_pk_tab;
+    E.cus = c->cus;
+    E.lognbits = -1;
+    for (int s = 0; s < 8; ++s)
+        if ((8u * nbytes) == (1u << s)) E.lognbits = s;
     E.data = data, E.nbytes = nbytes, E.masks = masks;
     E.out = batch_arg(out);
     E.n = out->n;
     E.status = c->d_status;
     fill_bounds(E.ob, out);
+    E.uniform_cap = 1;
+    for (uint32_t i = 0, o = 0; i < out->nbits; ++i) {
+        E.ooff.b[i] = o, o += cap_of(out->bound[i]);
+        E.uniform_cap &= cap_of(out->bound[i]) == c->pk_cap;
+    }
     DeviceGuard g(c->device);
     int r = launch_encrypt(E, c->stream);
     if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
@@ -548,6 +586,9 @@ hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) {
         o += cap_of(in->bound[i]);
         D.maxcap = std::max(D.maxcap, cap_of(in->bound[i]));
     }
+    D.ucap = cap_of(in->bound[0]) <= 8 ? cap_of(in->bound[0]) : 0;
+    for (uint32_t i = 1; i < in->nbits; ++i)
+        if (cap_of(in->bound[i]) != D.ucap) D.ucap = 0;
     DeviceGuard g(c->device);
     return launch_decrypt(D, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }

@@ -47,15 +47,20 @@ struct AddArgs {
 };
 
 struct EncArgs {
-    const uint64_t *pk; // tau * pk_cap limbs
+    const uint64_t *pk;     // tau * pk_cap limbs
+    const uint64_t *pk_tab; // nibble table [ceil(tau/4)][limb pair][16][2] (upload_pk), or null
+    uint32_t cus;           // compute units (grid sizing)
     uint32_t tau, pk_cap;
     const uint8_t *data;
     uint32_t nbytes;
+    int lognbits;           // log2(8*nbytes) when a power of two, else -1
+    uint32_t uniform_cap;   // every output bit has exactly pk_cap limbs: stores go through LDS
     const uint8_t *masks;
     BatchArg out;
     uint64_t n;
     int *status;
     Bounds ob;
+    Bounds ooff;            // limb offset of each bit within a value (prefix sums of the caps)
 };
 
 struct DecArgs {
@@ -69,6 +74,7 @@ struct DecArgs {
     Bounds ib;
     Bounds ioff;     // limb offset of each bit within a value (prefix sums of the caps)
     uint32_t maxcap; // widest bit (limbs): picks lane-per-bit or wave-per-value
+    uint32_t ucap;   // every bit has exactly ucap <= 8 limbs (fresh ciphertexts), else 0
 };
 
 // Gates and the carry-save multiplier keep their intermediates in a per-value global workspace.
@@ -125,5 +131,6 @@ int launch_poly_mul(const PolyArgs &a, void *stream);
 int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
+constexpr size_t kEncTableBytes = 64 * 1024; // largest encryption nibble table staged in LDS
 
 } // namespace hm

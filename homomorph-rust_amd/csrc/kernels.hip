@@ -890,9 +890,145 @@ __global__ void __launch_bounds__(256) encrypt_kernel(EncArgs E) {
     E.out.degree[e * nbits + k] = (uint32_t)deg;
 }
 
+// Table form of the same subset sum (four Russians over the mask): the public-key rows are taken
+// four at a time, with the 16 XOR combinations of every group precomputed per key (upload_pk:
+// T[g][n] = XOR_{k : bit k of n} T_{4g+k}).  Each block copies that table into LDS once and its
+// threads stride over ciphertext bits; a bit is one LDS lookup per mask nibble -- tau/4 lookups
+// of PC limbs instead of tau masked XORs of PC limbs with a scalar (SGPR) operand, which run at
+// ~0.6 rate.  Same output bits: XOR is associative and commutative.
+constexpr int kEncBlock = 512;
+
+// one nibble lookup: acc ^= T[g][nib] (NP limb pairs, one conflict-free ds_read_b128 each)
+template <int NP>
+__device__ __forceinline__ void enc_lookup(uint64_t *acc, const uint4 *tab4, uint32_t g,
+                                           uint32_t nib) {
+    const uint4 *row = tab4 + (size_t)g * NP * 16 + nib;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const uint4 v = row[p * 16];
+        acc[2 * p] ^= (uint64_t)v.x | ((uint64_t)v.y << 32);
+        acc[2 * p + 1] ^= (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+}
+
+// GC: compile-time group count (tau/4) for the fully unrolled path with 16-byte-aligned masks
+// (tau = 128: one uint4 of mask per ciphertext bit), 0 = any tau
+template <int PC, int GC>
+__global__ void __launch_bounds__(kEncBlock) encrypt_table_kernel(EncArgs E) {
+    constexpr int NP = (PC + 1) / 2;  // limb pairs
+    extern __shared__ uint64_t tab[]; // [G][NP][16][2] (upload_pk)
+    const uint32_t G = GC ? GC : (E.tau + 3) / 4;
+    {
+        const uint32_t n16 = G * NP * 16; // 16-byte chunks
+        const uint4 *src = (const uint4 *)E.pk_tab;
+        uint4 *dst = (uint4 *)tab;
+        for (uint32_t f = threadIdx.x; f < n16; f += blockDim.x) dst[f] = src[f];
+    }
+    __syncthreads();
+    const uint4 *tab4 = (const uint4 *)tab;
+    uint64_t *stage = tab + (size_t)G * NP * 32; // [waves][64][PC] store transpose
+    const uint32_t nbits = E.nbytes * 8;
+    const uint32_t mb = (E.tau + 7) / 8;
+    const uint64_t total = E.n * nbits;
+    // the loop runs per wave (the store transpose is wave-cooperative): lanes past the end of
+    // the batch compute on a clamped index and are masked out of every store
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); t0 < total;
+         t0 += step) {
+        const bool live = t0 + lane < total;
+        const uint64_t t = live ? t0 + lane : total - 1;
+        const uint64_t e = E.lognbits >= 0 ? t >> E.lognbits : t / nbits;
+        const uint32_t k = (uint32_t)(t - e * nbits);
+        const uint8_t *m = E.masks + t * mb;
+        uint64_t acc[2 * NP];
+#pragma unroll
+        for (int l = 0; l < 2 * NP; ++l) acc[l] = 0;
+        if constexpr (GC != 0) {
+            static_assert(GC % 32 == 0, "GC: whole uint4 mask words");
+#pragma unroll
+            for (int w4 = 0; w4 < GC / 32; ++w4) {
+                const uint4 mw = ((const uint4 *)m)[w4];
+                const uint32_t ws[4] = {mw.x, mw.y, mw.z, mw.w};
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        enc_lookup<NP>(acc, tab4, 32 * w4 + 8 * w + j, (ws[w] >> (4 * j)) & 15u);
+            }
+        } else {
+            for (uint32_t g0 = 0; g0 < G; g0 += 8) { // one 32-bit mask word = 8 nibbles
+                const uint32_t b0 = g0 / 2;           // first mask byte of this word
+                uint32_t bits;
+                if ((mb & 3u) == 0) {
+                    bits = *(const uint32_t *)(m + b0);
+                } else {
+                    bits = 0;
+                    for (uint32_t b = 0; b < 4 && b0 + b < mb; ++b)
+                        bits |= (uint32_t)m[b0 + b] << (8 * b);
+                }
+                const uint32_t ng = min(8u, G - g0);
+                for (uint32_t j = 0; j < ng; ++j)
+                    enc_lookup<NP>(acc, tab4, g0 + j, (bits >> (4 * j)) & 15u);
+            }
+        }
+        // mask bits at or above tau select nothing: the table rows past tau are zero, and the
+        // reference reads exactly ceil(tau/8) bytes, bits >= tau unused (cipher.rs:105-110)
+        acc[0] ^= (E.data[e * E.nbytes + k / 8] >> (k % 8)) & 1u; // add_bool_assign (:112)
+        int deg = 0;
+#pragma unroll
+        for (int l = 0; l < PC; ++l)
+            if (acc[l]) deg = l * 64 + 63 - __builtin_clzll(acc[l]);
+        if (live) {
+            if ((uint32_t)deg > E.ob.b[k]) flag(E.status, HM_ERR_CAPACITY);
+            E.out.degree[e * nbits + k] = (uint32_t)deg;
+        }
+        if (E.uniform_cap) {
+            // the wave's 64 bits own 64*PC consecutive output limbs (limb l of bit t at t*PC + l):
+            // transpose through LDS and store them coalesced (lane j writes limb j, j + 64, ...)
+            uint64_t *st = stage + (size_t)(threadIdx.x & ~63u) * PC;
+#pragma unroll
+            for (int l = 0; l < PC; ++l) st[lane * PC + l] = acc[l];
+            wsync();
+            const uint64_t lim = (total - t0) * PC;
+            uint64_t *dst = E.out.limbs + t0 * PC;
+#pragma unroll
+            for (int r = 0; r < PC; ++r) {
+                const uint32_t j = lane + 64 * r;
+                if (j < lim) dst[j] = st[j];
+            }
+            wsync();
+        } else if (live) {
+            const uint32_t cap = cap_of(E.ob.b[k]);
+            uint64_t *dst = E.out.limbs + e * E.out.stride + E.ooff.b[k];
+#pragma unroll
+            for (int l = 0; l < PC; ++l) {
+                if ((uint32_t)l < cap) dst[l] = acc[l];
+                else if (acc[l]) flag(E.status, HM_ERR_CAPACITY);
+            }
+            for (uint32_t l = PC; l < cap; ++l) dst[l] = 0ull;
+        }
+    }
+}
+
 template <int PC>
 static void launch_enc_pc(const EncArgs &E, void *stream) {
     const uint64_t threads = E.n * E.nbytes * 8;
+    const size_t tab = (size_t)((E.tau + 3) / 4) * ((PC + 1) / 2) * 16 * 16;
+    const size_t lds = tab + (size_t)kEncBlock * PC * 8; // + the store transpose
+    if (E.pk_tab && tab <= kEncTableBytes && lds <= 64 * 1024 && !getenv("HM_ENC_PLAIN")) {
+        // a few resident blocks per CU, each striding over bits (the table copy is amortised)
+        const uint64_t want = (threads + kEncBlock - 1) / kEncBlock;
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
+        const uint64_t blocks = std::min<uint64_t>(want, (uint64_t)E.cus * per_cu);
+        if (E.tau == 128 && ((uintptr_t)E.masks & 15u) == 0)
+            hipLaunchKernelGGL((encrypt_table_kernel<PC, 32>), dim3((unsigned)blocks),
+                               dim3(kEncBlock), lds, (hipStream_t)stream, E);
+        else
+            hipLaunchKernelGGL((encrypt_table_kernel<PC, 0>), dim3((unsigned)blocks),
+                               dim3(kEncBlock), lds, (hipStream_t)stream, E);
+        return;
+    }
     const uint64_t blocks = (threads + 255) / 256;
     hipLaunchKernelGGL(encrypt_kernel<PC>, dim3((unsigned)blocks), dim3(256), 0,
                        (hipStream_t)stream, E);
@@ -973,7 +1109,25 @@ __global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t total = D.n * D.nbits;
     uint32_t p = 0;
-    if (g < total) {
+    if (D.ucap) {
+        // uniform caps: the wave's 64 bits are 64*C consecutive limbs (bit g at g*C).  Load them
+        // coalesced into LDS, then each lane folds its own C limbs.
+        __shared__ uint64_t st[256 * 8];
+        const uint32_t C = D.ucap, lane = threadIdx.x & 63u;
+        uint64_t *sw = st + (threadIdx.x & ~63u) * C;
+        const uint64_t g0 = g - lane, lim = g0 < total ? (total - g0) * C : 0;
+        const uint64_t *src = D.in.limbs + g0 * C;
+        for (uint32_t j = lane; j < 64 * C; j += 64)
+            if (j < lim) sw[j] = src[j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (g < total) {
+            uint64_t acc = 0;
+            for (uint32_t l = 0; l < C; ++l) acc ^= sw[lane * C + l] & D.z[l];
+            p = (uint32_t)__builtin_popcountll(acc) & 1u;
+        }
+    } else if (g < total) {
         const uint64_t e = g / D.nbits;
         const uint32_t k = (uint32_t)(g % D.nbits);
         const uint64_t *src = D.in.limbs + e * D.in.stride + D.ioff.b[k];

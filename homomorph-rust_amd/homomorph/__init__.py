@@ -353,11 +353,29 @@ class Context:
 
     def _launch(self, fn, what: str):
         torch = _torch()
+        if torch.cuda.is_current_stream_capturing():
+            _check(fn(), what)  # inside Context.graph: the engine stream is the capture stream
+            return
         cur = torch.cuda.current_stream(self.device)
         self._stream.wait_stream(cur)
         st = fn()
         cur.wait_stream(self._stream)
         _check(st, what)
+
+    def graph(self, fn, warmup: int = 1):
+        """Capture the engine launches `fn` makes into one HIP graph on the engine stream and
+        return it (a torch.cuda.CUDAGraph; `.replay()` re-runs it on the current stream, over the
+        same buffers).  `fn` runs `warmup` times first, so that workspaces and decrypt tables are
+        allocated outside the capture; launch-bound sequences (encrypt + decrypt of a batch) then
+        cost one graph launch instead of one host round trip per kernel."""
+        torch = _torch()
+        for _ in range(warmup):
+            fn()
+        self.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self._stream):
+            fn()
+        return g
 
     @property
     def stream(self):
