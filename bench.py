@@ -10,16 +10,24 @@ region the decrypted results are gathered over RCCL (all_gather) and checked on 
 `--workload mixed` runs configs[4] instead: one u32 add plus one u32 multiply (low 8 result bits)
 per value at d = dp = tau = 256, global batch 2^20 split over the ranks (strong scaling).
 
+`--gpus N` with N > 1 and no torchrun environment starts N rank processes itself (one per GPU,
+before this process touches the GPU) and exits with their status; under torchrun it checks that
+WORLD_SIZE equals N.  `--workload distcheck` runs only the multi-rank plumbing (spawn, key
+broadcast, shards, result gather, max-over-ranks time) on the CPU with gloo, for the CPU tests.
+
 Prints ONE JSON line (rank 0).  Besides the contract fields it carries
   roofline      HBM roofline of the add kernel: algorithmic bytes per launch / kernel time
   cpu_baseline  the CPU oracle (operation-for-operation restatement of the reference) timed on a
-                bounded sample on this host, single thread (the reference is single-threaded)
-  secondary     u32 encrypt+decrypt throughput (configs[2]) and u8 multiply throughput (the
-                feasible form of configs[3]; a full u32 mul is infeasible)
+                bounded sample on this host: one thread (the reference is single-threaded) and
+                all host cores (values split over OpenMP threads), CPU model stated
+  secondary     u32 encrypt+decrypt throughput (configs[2]) and multiply throughput (u8, and the
+                low result bits of the u32 circuit; a full u32 mul is infeasible)
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,23 +50,59 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def setup_dist(gpus):
+def spawn_ranks(args):
+    """`bench.py --gpus N` outside torchrun: start N rank processes of this same script (one per
+    GPU; RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) and return their exit status.
+    Runs before anything here touches the GPU; a rank that fails takes the others down."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:  # the exact child PIDs this process started
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.workload == "distcheck":  # CPU plumbing only: gloo, no GPU
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        return world, rank, local, torch.device("cpu")
+    # one rank per GPU; HM_BENCH_BACKEND=gloo with more ranks than GPUs is a rehearsal mode for
+    # a one-GPU box (ranks share the card), never the measured configuration
+    backend = os.environ.get("HM_BENCH_BACKEND", "nccl")
+    dev = local % torch.cuda.device_count() if backend == "gloo" else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        # one rank per GPU; HM_BENCH_BACKEND=gloo with more ranks than GPUs is a rehearsal mode
-        # for a one-GPU box (ranks share the card), never the measured configuration
-        backend = os.environ.get("HM_BENCH_BACKEND", "nccl")
-        dev = local % torch.cuda.device_count() if backend == "gloo" else local
-        torch.cuda.set_device(dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    return world, rank, local
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: {dist.get_world_size()} ranks joined, --gpus {args.gpus}")
+    return world, rank, local, torch.device("cuda", dev)
 
 
 def barrier(world):
@@ -88,7 +132,7 @@ def make_context(world, rank, device, params=PARAMS):
     ctx = H.Context(H.Parameters(*params), device=device)
     sk = pk = None
     if rank == 0:
-        ctx.seed_rng(0xB0B)
+        ctx.seed_rng(0xB0B)  # reproducible keys and masks (the test contract)
         ctx.generate_secret_key()
         ctx.generate_public_key()
         sk, pk = ctx.get_secret_key().limbs, ctx.get_public_key().limbs
@@ -144,41 +188,79 @@ def time_loop(fn, steps, warmup, world, stream=None):
     return wall, ev0.elapsed_time(ev1) / 1e3
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores():
+    """CPUs this process may use (the GPU box's share; os.cpu_count() shows the whole host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
 def cpu_baseline_add(seconds):
-    """Oracle (C restatement of the reference's add path) on one host core, bounded sample."""
+    """Oracle (C restatement of the reference's add path) on a bounded sample of the configs[1]
+    workload: one thread (comparable with the single-threaded reference) and all host cores
+    (values split over OpenMP threads)."""
     from oracle import oracle_py as oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import as_bytes, fresh_bound, keys, masks
     d, dp, delta, tau = PARAMS
     sk, pk, _ = keys(d, dp, delta, tau, 77)
+    cores = host_cores()
+    n = max(4, cores)
     rng = np.random.default_rng(5)
-    n = 4
     a = rng.integers(0, 2**32, size=n, dtype=np.uint32)
     b = rng.integers(0, 2**32, size=n, dtype=np.uint32)
     bound = fresh_bound(d, dp, 32)
     la, da = oracle.encrypt_batch(pk, as_bytes(a), masks(n, 32, tau, 1), bound)
     lb, db = oracle.encrypt_batch(pk, as_bytes(b), masks(n, 32, tau, 2), bound)
     ob = H.add_out_bounds(bound, bound)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        oracle.add_batch(la, da, bound, lb, db, bound, 32, n, ob)
-        done += n
-    el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "adds/s", "cores": 1, "kind": "port",
-            "sample": f"{done} u32 homomorphic adds (4 seeded pairs, repeated) in {el:.1f} s, "
-                      f"C oracle restating src/polynomial.rs + common.rs, 1 thread, -O3"}
+
+    def leg(threads, secs, per_call):
+        oracle.set_threads(threads)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            oracle.add_batch(la[: per_call * len(la) // n], da[: per_call * 32], bound,
+                             lb[: per_call * len(lb) // n], db[: per_call * 32], bound, 32,
+                             per_call, ob)
+            done += per_call
+        el = time.perf_counter() - t0
+        oracle.set_threads(1)
+        return done, el
+
+    d1, e1 = leg(1, seconds * 0.6, 4)
+    dn, en = leg(cores, seconds * 0.4, n)
+    return {"value": d1 / e1, "unit": "adds/s", "cores": 1, "kind": "port",
+            "cpu": cpu_model(), "host_cores_available": cores,
+            "sample": f"{d1} u32 homomorphic adds (4 seeded pairs, repeated) in {e1:.1f} s on 1 "
+                      f"thread; C oracle restating src/polynomial.rs + common.rs, -O3",
+            "all_cores": {"value": dn / en, "unit": "adds/s", "cores": cores,
+                          "sample": f"{dn} adds ({n} seeded pairs per call, values split over "
+                                    f"{cores} OpenMP threads) in {en:.1f} s"}}
 
 
 def secondary_metrics(ctx, device, steps):
     out = {}
-    # configs[2]: u32 encrypt + decrypt, batch 65536 (masks drawn on device, inputs resident)
+    # configs[2]: u32 encrypt + decrypt, batch 65536.  Like the reference (whose encryption
+    # draws its subset masks from getrandom), each step draws fresh masks from the engine's
+    # CSPRNG (device ChaCha20) inside the timed step; the same pair over pre-drawn masks is
+    # reported beside it.
     n = 65536
-    tau = PARAMS[3]
-    gen = torch.Generator(device=device)
-    gen.manual_seed(7)
-    vals = torch.randint(0, 2**31, (n,), dtype=torch.int64, device=device).to(torch.int32)
+    vals = torch.from_numpy(np.random.default_rng(7).integers(0, 2**32, size=n, dtype=np.uint32)
+                            .view(np.int32)).to(device)
     data = vals.view(torch.uint8).reshape(n, 4)
-    m = torch.randint(0, 256, (n, 32, (tau + 7) // 8), dtype=torch.uint8, device=device, generator=gen)
+    m = ctx.random_bytes(n * 32 * ctx.mask_bytes())
     bound = np.full(32, ctx.fresh_bound(), dtype=np.uint32)
     c = H.Ciphered.empty(n, bound, device)
     dec = torch.empty((n, 4), dtype=torch.uint8, device=device)
@@ -186,22 +268,28 @@ def secondary_metrics(ctx, device, steps):
     L = H.lib()
     import ctypes
 
-    def encdec():
-        ctx._launch(lambda: L.hm_encrypt_batch(ctx._h, data.data_ptr(), 4, m.data_ptr(),
+    def encdec(masks_ptr):
+        ctx._launch(lambda: L.hm_encrypt_batch(ctx._h, data.data_ptr(), 4, masks_ptr,
                                                ctypes.byref(cb))
                     | L.hm_decrypt_batch(ctx._h, ctypes.byref(cb), dec.data_ptr()), "enc+dec")
 
-    # the pair is launch-bound (~65 us of kernels): replay it as one captured HIP graph
-    g = ctx.graph(encdec, warmup=2)
     reps = max(20, 5 * steps)
-    dec.zero_()
-    wall, ev_s = time_loop(g.replay, reps, 2, 1)
-    ctx.synchronize()
-    ok = bool(torch.equal(dec, data))
-    out["u32_encrypt_decrypt"] = {"value": n * reps / wall, "unit": "u32 enc+dec/s",
-                                  "batch": n, "verified": ok, "steps": reps,
-                                  "kernel_us_per_step": 1e6 * ev_s / reps,
-                                  "launch": "one HIP graph replay per step (encrypt + decrypt)"}
+    res = {}
+    for key, mp in (("csprng", None), ("predrawn", m.data_ptr())):
+        # the pair is launch-bound (~65 us of kernels): replay it as one captured HIP graph
+        g = ctx.graph(lambda: encdec(mp), warmup=2)
+        dec.zero_()
+        wall, ev_s = time_loop(g.replay, reps, 2, 1)
+        ctx.synchronize()
+        res[key] = (n * reps / wall, bool(torch.equal(dec, data)), 1e6 * ev_s / reps)
+    out["u32_encrypt_decrypt"] = {
+        "value": res["csprng"][0], "unit": "u32 enc+dec/s", "batch": n,
+        "verified": res["csprng"][1] and res["predrawn"][1], "steps": reps,
+        "kernel_us_per_step": res["csprng"][2],
+        "masks": "drawn per step from the engine CSPRNG (ChaCha20 on device), as the "
+                 "reference's getrandom draw is part of its encryption",
+        "predrawn_masks": {"value": res["predrawn"][0], "kernel_us_per_step": res["predrawn"][2]},
+        "launch": "one HIP graph replay per step (mask draw + encrypt + decrypt)"}
 
     # PCIe-inclusive add rate: the same 4096-value add with its inputs copied host->device and
     # its outputs device->host (pinned buffers) inside every step -- what a caller handing host
@@ -268,9 +356,7 @@ def run_add(args, world, rank, device):
     ctx = make_context(world, rank, device)
     n = args.batch or 4096
     a, b = shard_inputs(rank, n)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(31 + rank)
-    ca, cb = ctx.encrypt(a, generator=gen), ctx.encrypt(b, generator=gen)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)  # masks from the (seeded) engine CSPRNG
     ob = H.add_out_bounds(ca.bound, cb.bound)
     out = H.Ciphered.empty(n, ob, device, np.dtype(np.uint32))
     ctx.synchronize()
@@ -314,7 +400,7 @@ def run_add(args, world, rank, device):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic: seeded u32 plaintexts, seeded keys, device-drawn subset masks",
+        "data": "synthetic: seeded u32 plaintexts, seeded keys, subset masks from the seeded engine CSPRNG",
         "config": {"workload": "u32 homomorphic add (configs[1])", "global_batch": n * world,
                    "batch_per_gpu": n, "d": PARAMS[0], "dp": PARAMS[1], "delta": PARAMS[2],
                    "tau": PARAMS[3], "parallelism": f"batch-sharded x{world}"},
@@ -347,9 +433,7 @@ def run_mixed(args, world, rank, device):
         raise SystemExit("--batch must divide by the number of ranks")
     n = glob // world
     a, b = shard_inputs(rank, n)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(31 + rank)
-    ca, cb = ctx.encrypt(a, generator=gen), ctx.encrypt(b, generator=gen)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)  # masks from the (seeded) engine CSPRNG
     sums = H.Ciphered.empty(n, H.add_out_bounds(ca.bound, cb.bound), device, np.dtype(np.uint32))
     kb = H.mul_out_bounds(ca.bound[:MUL_LOW_K], cb.bound[:MUL_LOW_K])
     prods = H.Ciphered.empty(n, kb, device, np.dtype(np.uint8))
@@ -387,7 +471,7 @@ def run_mixed(args, world, rank, device):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic: seeded u32 plaintexts, seeded keys, device-drawn subset masks",
+        "data": "synthetic: seeded u32 plaintexts, seeded keys, subset masks from the seeded engine CSPRNG",
         "config": {"workload": "u32 mixed add+mul (configs[4])", "global_batch": glob,
                    "batch_per_gpu": n, "launch_chunk": MIXED_CHUNK, "d": MIXED_PARAMS[0],
                    "dp": MIXED_PARAMS[1], "delta": MIXED_PARAMS[2], "tau": MIXED_PARAMS[3],
@@ -398,16 +482,39 @@ def run_mixed(args, world, rank, device):
     }
 
 
+def run_distcheck(args, world, rank, device):
+    """The multi-rank plumbing alone, on the CPU (gloo): rank 0's keys reach every rank, each
+    rank owns a distinct shard, results are gathered in rank order and the time is the max over
+    ranks.  No engine call: the CPU tests drive `bench.py --gpus 2 --workload distcheck`."""
+    n = args.batch or 64
+    sk = pk = None
+    if rank == 0:
+        rng = np.random.default_rng(0xB0B)
+        sk = rng.integers(0, 2**63, size=3, dtype=np.uint64)
+        pk = rng.integers(0, 2**63, size=(PARAMS[3], 5), dtype=np.uint64)
+    t0 = time.perf_counter()
+    sk, pk = broadcast_keys(world, rank, device, sk, pk)
+    a, b = shard_inputs(rank, n)
+    res = torch.from_numpy((a + b).astype(np.uint32).view(np.uint8).reshape(n, 4).copy())
+    got, wall = gather_results(world, device, res, time.perf_counter() - t0 + rank)
+    want = np.concatenate([sum(shard_inputs(r, n)).astype(np.uint32) for r in range(world)])
+    digest = int(np.bitwise_xor.reduce(pk.reshape(-1))) ^ int(np.bitwise_xor.reduce(sk))
+    return {"metric": "distcheck", "value": float(n * world), "unit": "values gathered",
+            "n_gpus": world, "world_size_seen": dist.get_world_size() if world > 1 else 1,
+            "gathered_ok": bool(np.array_equal(got.view("<u4").reshape(-1), want)),
+            "max_wall_s": wall, "key_digest": digest}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["add", "mixed"], default="add",
-                    help="add: configs[1] (headline); mixed: configs[4]")
+    ap.add_argument("--workload", choices=["add", "mixed", "distcheck"], default="add",
+                    help="add: configs[1] (headline); mixed: configs[4]; distcheck: CPU plumbing")
     ap.add_argument("--batch", type=int, default=0,
                     help="add: u32 pairs per GPU (default 4096); mixed: global batch (2^20)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--graph", type=int, default=1,
@@ -415,12 +522,14 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "add_traffic.json"),
                     help="PMC-derived HBM bytes per add launch (scripts/traffic_json.py)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
 
-    world, rank, local = setup_dist(args.gpus)
-    device = torch.device("cuda", torch.cuda.current_device())
-    run = run_add if args.workload == "add" else run_mixed
+    world, rank, local, device = setup_dist(args)
+    run = {"add": run_add, "mixed": run_mixed, "distcheck": run_distcheck}[args.workload]
     result = run(args, world, rank, device)
     if rank == 0:
+        result.setdefault("world_size_seen", dist.get_world_size() if world > 1 else 1)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

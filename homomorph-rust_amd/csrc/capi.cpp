@@ -11,8 +11,9 @@
 #include <cstring>
 #include <mutex>
 #include <new>
-#include <random>
 #include <vector>
+
+#include <sys/random.h>
 
 #include "engine.h"
 #include "gf2_wave.h"
@@ -24,7 +25,14 @@ struct hm_ctx {
     int device;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    // Randomness.  Unseeded (the default): key polynomials come straight from getrandom(2), as
+    // Polynomial::random does (src/polynomial.rs:73-96), and encryption masks from a device
+    // ChaCha20 keystream keyed with 32 getrandom bytes.  hm_ctx_seed_rng switches both to a
+    // reproducible test contract: SplitMix64 for keys, a ChaCha20 key derived from the seed.
+    bool seeded = false;
     uint64_t rng = 0;
+    uint32_t chacha_key[8] = {};
+    uint64_t *d_nonce = nullptr;       // device ChaCha20 nonce counter, advanced by every draw
     // keys (host copies; SecretKey / PublicKey)
     bool has_sk = false, has_pk = false;
     std::vector<uint64_t> sk;          // limbs of S
@@ -42,9 +50,24 @@ struct hm_ctx {
     size_t ws_bytes = 0;
     uint32_t *d_ws_add = nullptr;      // adder workspace (validated inputs, per-bit a_i*b_i)
     size_t ws_add_bytes = 0;
+    uint32_t *d_mws = nullptr;         // column multiplier arena (mul_columns)
+    size_t mws_bytes = 0;
+    uint8_t *d_masks = nullptr;        // engine-drawn encryption masks (hm_encrypt_batch, masks NULL)
+    size_t masks_bytes = 0;
     int *d_status = nullptr;
     uint32_t cus = 256;                // compute units of the device (grid sizing)
     hipError_t last_hip = hipSuccess;
+    // Device buffers the kernels read are never freed while the context lives: a HIP graph
+    // captured over the engine's launches holds their raw pointers.  A buffer that has to be
+    // replaced (grown, or keyed by a new key) is retired instead -- zeroed first when it holds
+    // secret-derived data -- and `generation` advances, so a graph wrapper can refuse to replay
+    // across the change (hm_ctx_generation).  hm_ctx_trim / hm_ctx_destroy free retired buffers.
+    struct Retired {
+        void *p;
+        size_t bytes;
+    };
+    std::vector<Retired> retired;
+    uint64_t generation = 0;
 };
 
 namespace {
@@ -78,13 +101,58 @@ size_t degree_of(const uint64_t *c, size_t n) {
     return 0;
 }
 
-// Polynomial::random(degree) (src/polynomial.rs:73-96) from the context stream.
-std::vector<uint64_t> random_poly(size_t degree, uint64_t &st) {
-    std::vector<uint64_t> v(degree / 64 + 1);
-    for (auto &w : v) w = splitmix64(st);
+// getrandom(2) into buf (the reference's getrandom::fill, src/polynomial.rs:87, cipher.rs:95)
+bool os_random(void *buf, size_t n) {
+    uint8_t *p = (uint8_t *)buf;
+    while (n) {
+        const ssize_t r = getrandom(p, n, 0);
+        if (r < 0) return false;
+        p += r, n -= (size_t)r;
+    }
+    return true;
+}
+
+// Polynomial::random(degree) (src/polynomial.rs:73-96): limbs from getrandom, or from the
+// context's SplitMix64 stream once hm_ctx_seed_rng fixed it (test contract); top bit forced,
+// bits above it cleared (:89-90).
+bool random_poly(hm_ctx *c, size_t degree, std::vector<uint64_t> &v) {
+    v.assign(degree / 64 + 1, 0);
+    if (c->seeded) {
+        for (auto &w : v) w = splitmix64(c->rng);
+    } else if (!os_random(v.data(), v.size() * 8)) {
+        return false;
+    }
     v.back() &= (1ull << (degree % 64)) - 1;
     v.back() |= 1ull << (degree % 64);
-    return v;
+    return true;
+}
+
+void wipe(void *p, size_t n) {
+    volatile uint8_t *q = (volatile uint8_t *)p;
+    for (size_t i = 0; i < n; ++i) q[i] = 0;
+}
+
+void retire(hm_ctx *c, void *p, size_t bytes, bool secret) {
+    if (!p) return;
+    if (secret) (void)hipMemset(p, 0, bytes); // SecretKey's Drop zeroizes (context.rs:197-206)
+    c->retired.push_back({p, bytes});
+    ++c->generation;
+}
+
+// Grow-only device buffer (see hm_ctx::retired).  Allocation is synchronous, outside any
+// capture: callers size buffers on a warm-up call before a graph is captured.
+template <class T>
+hipError_t grow(hm_ctx *c, T *&p, size_t &have, size_t need, bool secret = false) {
+    if (need <= have && p) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    retire(c, p, have, secret);
+    p = nullptr, have = 0;
+    e = hipMalloc(&p, need);
+    if (e != hipSuccess) return e;
+    have = need;
+    ++c->generation;
+    return hipSuccess;
 }
 
 // Host carry-less product for key generation only (setup path, runs once per key).
@@ -158,8 +226,9 @@ bool covers(const hm_batch *out, const std::vector<uint32_t> &need) {
 // conflict-free ds_read_b128 -- 16 distinct addresses cover the 64 LDS banks exactly once.
 hm_status upload_pk(hm_ctx *c) {
     DeviceGuard g(c->device);
-    if (c->d_pk) (void)hipFree(c->d_pk), c->d_pk = nullptr;
-    if (c->d_pk_tab) (void)hipFree(c->d_pk_tab), c->d_pk_tab = nullptr;
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    retire(c, c->d_pk, 0, false), c->d_pk = nullptr;
+    retire(c, c->d_pk_tab, 0, false), c->d_pk_tab = nullptr;
     HM_HIP(c, hipMalloc(&c->d_pk, c->pk.size() * 8));
     HM_HIP(c, hipMemcpy(c->d_pk, c->pk.data(), c->pk.size() * 8, hipMemcpyHostToDevice));
     const uint32_t G = (c->pk_tau + 3) / 4, PC = c->pk_cap, NP = (PC + 1) / 2;
@@ -187,8 +256,8 @@ void drop_secret(hm_ctx *c) {
     }
     c->sk.clear();
     if (c->d_z) {
-        (void)hipMemset(c->d_z, 0, (size_t)c->z_limbs * 8);
-        (void)hipFree(c->d_z);
+        (void)hipStreamSynchronize(c->stream);
+        retire(c, c->d_z, (size_t)c->z_limbs * 8, true);
         c->d_z = nullptr;
         c->z_limbs = 0;
     }
@@ -220,17 +289,26 @@ hm_status ensure_ztable(hm_ctx *c, uint32_t max_bound) {
             for (size_t w = 0; w < sl; ++w) r[w] ^= c->sk[w];
     }
     DeviceGuard g(c->device);
-    if (c->d_z) {
-        (void)hipMemset(c->d_z, 0, (size_t)c->z_limbs * 8);
-        (void)hipFree(c->d_z);
-        c->d_z = nullptr;
-    }
-    HM_HIP(c, hipMalloc(&c->d_z, (size_t)need * 8));
+    size_t have = (size_t)c->z_limbs * 8;
+    HM_HIP(c, grow(c, c->d_z, have, (size_t)need * 8, true));
     HM_HIP(c, hipMemcpy(c->d_z, z.data(), (size_t)need * 8, hipMemcpyHostToDevice));
-    volatile uint64_t *pz = z.data();
-    for (size_t i = 0; i < z.size(); ++i) pz[i] = 0;
+    wipe(z.data(), z.size() * 8);
+    wipe(r.data(), r.size() * 8);
     c->z_limbs = need;
     return HM_OK;
+}
+
+// n bytes of the context's ChaCha20 keystream into device memory: the kernel reads the nonce
+// from device memory and a second launch advances it, so every draw -- also every replay of a
+// captured graph that contains one -- uses a fresh keystream (DESIGN.md "Randomness").
+hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n) {
+    if (!n) return HM_OK;
+    RandArgs R{};
+    std::memcpy(R.key, c->chacha_key, sizeof(R.key));
+    R.nonce = c->d_nonce, R.out = dst, R.nbytes = n;
+    const int r = launch_random(R, c->stream);
+    wipe(R.key, sizeof(R.key));
+    return r ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 
 hm_status check_batch(const hm_batch *b, bool need_limbs = true) {
@@ -260,6 +338,7 @@ const char *hm_status_string(hm_status s) {
     case HM_ERR_INVALID_ARGUMENT: return "invalid argument";
     case HM_ERR_INVALID_CIPHERED_LENGTH: return "ciphered length is not a multiple of 8";
     case HM_ERR_BAD_INPUT: return "input degree does not match its limbs";
+    case HM_ERR_RANDOMNESS: return "the OS random source failed";
     }
     return "unknown status";
 }
@@ -274,14 +353,22 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
     hm_ctx *c = new (std::nothrow) hm_ctx();
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     c->d = d, c->dp = dp, c->delta = delta, c->tau = tau, c->device = device;
-    std::random_device rd; // OS randomness, as getrandom in the reference
-    c->rng = ((uint64_t)rd() << 32) ^ rd();
+    uint64_t nonce0 = 0;
+    if (!os_random(c->chacha_key, sizeof(c->chacha_key)) || !os_random(&nonce0, sizeof(nonce0))) {
+        delete c;
+        return HM_ERR_RANDOMNESS; // CipherError::Randomness (src/cipher.rs:18-24)
+    }
     DeviceGuard g(device);
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_status, sizeof(int));
     if (e == hipSuccess) e = hipMemset(c->d_status, 0, sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&c->d_nonce, sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMemcpy(c->d_nonce, &nonce0, sizeof(uint64_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
+        if (c->d_status) (void)hipFree(c->d_status);
+        if (c->d_nonce) (void)hipFree(c->d_nonce);
         if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+        wipe(c->chacha_key, sizeof(c->chacha_key));
         delete c;
         return HM_ERR_HIP;
     }
@@ -299,14 +386,27 @@ void hm_ctx_destroy(hm_ctx *c) {
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
     drop_secret(c);
-    if (c->d_pk) (void)hipFree(c->d_pk);
-    if (c->d_pk_tab) (void)hipFree(c->d_pk_tab);
-    if (c->d_s) (void)hipFree(c->d_s);
-    if (c->d_ws) (void)hipFree(c->d_ws);
-    if (c->d_ws_add) (void)hipFree(c->d_ws_add);
-    if (c->d_status) (void)hipFree(c->d_status);
+    if (c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
+    for (void *p : {(void *)c->d_pk, (void *)c->d_pk_tab, (void *)c->d_s, (void *)c->d_ws,
+                    (void *)c->d_ws_add, (void *)c->d_status, (void *)c->d_nonce,
+                    (void *)c->d_masks, (void *)c->d_mws})
+        if (p) (void)hipFree(p);
+    for (auto &r : c->retired) (void)hipFree(r.p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    wipe(c->chacha_key, sizeof(c->chacha_key));
+    wipe(&c->rng, sizeof(c->rng));
     delete c;
+}
+
+uint64_t hm_ctx_generation(const hm_ctx *c) { return c ? c->generation : 0; }
+
+hm_status hm_ctx_trim(hm_ctx *c) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    for (auto &r : c->retired) (void)hipFree(r.p);
+    c->retired.clear();
+    return HM_OK;
 }
 
 hm_status hm_ctx_set_stream(hm_ctx *c, void *s) {
@@ -350,41 +450,56 @@ hm_status hm_ctx_set_public_key(hm_ctx *c, const uint64_t *limbs, uint32_t tau, 
 
 hm_status hm_ctx_seed_rng(hm_ctx *c, uint64_t seed) {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
+    // test contract: keys from SplitMix64(seed), masks from ChaCha20 keyed by SplitMix64(seed ^ K)
+    c->seeded = true;
     c->rng = seed;
+    uint64_t ks = seed ^ 0x6D61736B73636861ull; // "masksCha"
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t w = splitmix64(ks);
+        c->chacha_key[2 * i] = (uint32_t)w, c->chacha_key[2 * i + 1] = (uint32_t)(w >> 32);
+    }
+    const uint64_t nonce0 = splitmix64(ks);
+    DeviceGuard g(c->device);
+    HM_HIP(c, hipMemcpyAsync(c->d_nonce, &nonce0, sizeof(nonce0), hipMemcpyHostToDevice, c->stream));
+    HM_HIP(c, hipStreamSynchronize(c->stream));
     return HM_OK;
 }
 
 hm_status hm_ctx_generate_secret_key(hm_ctx *c) { // src/context.rs:421-424
     if (!c) return HM_ERR_INVALID_ARGUMENT;
-    std::vector<uint64_t> s = random_poly(c->d, c->rng);
+    std::vector<uint64_t> s;
+    if (!random_poly(c, c->d, s)) return HM_ERR_RANDOMNESS;
     hm_status st = hm_ctx_set_secret_key(c, s.data(), s.size());
-    volatile uint64_t *p = s.data();
-    for (size_t i = 0; i < s.size(); ++i) p[i] = 0;
+    wipe(s.data(), s.size() * 8);
     return st;
 }
 
 hm_status hm_ctx_generate_public_key(hm_ctx *c) { // src/context.rs:249-261, :444-454
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
-    const uint32_t cap = ((uint32_t)c->d + c->dp) / 64 + 1;
-    std::vector<uint64_t> all((size_t)c->tau * cap, 0);
+    // T_i = S*Q_i + X*R_i.  deg S is d for generated keys but any degree for a key set with
+    // set_secret_key (the reference's own example, SecretKey::from_bytes(&[5, 14, 8]) at d = 6,
+    // has degree 19): rows are as wide as the widest T_i needs.
+    std::vector<std::vector<uint64_t>> rows(c->tau);
+    size_t cap = 1;
     for (uint32_t i = 0; i < c->tau; ++i) {
-        std::vector<uint64_t> q = random_poly(c->dp, c->rng);
-        std::vector<uint64_t> sq = clmul_host(c->sk, q);
-        std::vector<uint64_t> r = random_poly(c->delta, c->rng);
-        // X * R: shift left by one
-        std::vector<uint64_t> rx(r.size() + 1, 0);
-        for (size_t w = 0; w < r.size(); ++w) {
-            rx[w] |= r[w] << 1;
-            rx[w + 1] |= r[w] >> 63;
+        std::vector<uint64_t> q, r;
+        if (!random_poly(c, c->dp, q) || !random_poly(c, c->delta, r)) return HM_ERR_RANDOMNESS;
+        std::vector<uint64_t> t = clmul_host(c->sk, q);
+        t.resize(std::max(t.size(), r.size() + 1), 0);
+        for (size_t w = 0; w < r.size(); ++w) { // + X * R
+            t[w] ^= r[w] << 1;
+            t[w + 1] ^= r[w] >> 63;
         }
-        for (size_t w = 0; w < cap; ++w) {
-            uint64_t v = (w < sq.size() ? sq[w] : 0) ^ (w < rx.size() ? rx[w] : 0);
-            all[(size_t)i * cap + w] = v;
-        }
-        // anything above cap would mean deg T_i > d + dp, impossible by construction
+        wipe(q.data(), q.size() * 8);
+        wipe(r.data(), r.size() * 8);
+        cap = std::max(cap, (size_t)degree_of(t.data(), t.size()) / 64 + 1);
+        rows[i] = std::move(t);
     }
-    return hm_ctx_set_public_key(c, all.data(), c->tau, cap);
+    std::vector<uint64_t> all((size_t)c->tau * cap, 0);
+    for (uint32_t i = 0; i < c->tau; ++i)
+        for (size_t w = 0; w < cap && w < rows[i].size(); ++w) all[(size_t)i * cap + w] = rows[i][w];
+    return hm_ctx_set_public_key(c, all.data(), c->tau, (uint32_t)cap);
 }
 
 hm_status hm_ctx_get_secret_key(const hm_ctx *c, uint64_t *limbs, size_t cap, size_t *n) {
@@ -419,7 +534,15 @@ hm_status hm_validate_operation(const hm_ctx *c, hm_op op, uint16_t *req) {
     return HM_OK;
 }
 
-uint32_t hm_fresh_bound(const hm_ctx *c) { return c ? (uint32_t)c->d + c->dp : 0; }
+// A fresh ciphertext bit is a subset sum of public-key rows (plus the plaintext bit), so its
+// degree is at most max(d + dp, deg T_i): d + dp for generated keys, more for a loaded key.
+uint32_t hm_fresh_bound(const hm_ctx *c) {
+    if (!c) return 0;
+    const uint32_t b = (uint32_t)c->d + c->dp;
+    return c->has_pk ? std::max(b, c->pk_maxdeg) : b;
+}
+
+uint32_t hm_ctx_mask_bytes(const hm_ctx *c) { return (c && c->has_pk) ? (c->pk_tau + 7) / 8 : 0; }
 
 uint64_t hm_batch_stride(uint32_t nbits, const uint32_t *bound) {
     uint64_t s = 0;
@@ -537,10 +660,21 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     if (!c->has_pk) return HM_ERR_PUBLIC_KEY_UNSET;
     if (hm_status st = check_batch(out); st) return st;
     if (nbytes == 0 || out->nbits != 8 * nbytes) return HM_ERR_INVALID_ARGUMENT;
-    if (out->n && (!data || !masks)) return HM_ERR_INVALID_ARGUMENT;
+    if (out->n && !data) return HM_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < out->nbits; ++i)
         if (out->bound[i] < c->pk_maxdeg) return HM_ERR_INVALID_ARGUMENT;
     if (out->n == 0) return HM_OK;
+    DeviceGuard g(c->device);
+    if (!masks) {
+        // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): here the
+        // device ChaCha20 stream, drawn into the context's mask buffer right before the launch
+        const size_t mb = (size_t)out->n * out->nbits * ((c->pk_tau + 7) / 8);
+        const size_t need = (mb + 63) & ~(size_t)63;
+        if (need > c->masks_bytes && c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
+        HM_HIP(c, grow(c, c->d_masks, c->masks_bytes, need));
+        if (hm_status st = draw_random(c, c->d_masks, mb); st) return st;
+        masks = c->d_masks;
+    }
     EncArgs E{};
     E.pk = c->d_pk, E.tau = c->pk_tau, E.pk_cap = c->pk_cap;
     E.pk_tab = c->d_pk_tab;
@@ -558,10 +692,15 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
         E.ooff.b[i] = o, o += cap_of(out->bound[i]);
         E.uniform_cap &= cap_of(out->bound[i]) == c->pk_cap;
     }
-    DeviceGuard g(c->device);
     int r = launch_encrypt(E, c->stream);
     if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
+}
+
+hm_status hm_random_bytes(hm_ctx *c, uint8_t *dst, size_t nbytes) {
+    if (!c || (nbytes && !dst)) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    return draw_random(c, dst, nbytes);
 }
 
 hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) {
@@ -632,7 +771,6 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     {
         const uint64_t want = (16384 + a->n - 1) / a->n;
         A.wpv = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 8, (uint64_t)L}));
-        if (const char *w = getenv("HM_PREP_WPV")) A.wpv = std::max(1u, std::min((uint32_t)atoi(w), L));
         const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
         A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 4 * bpw);
         if ((size_t)A.prep_lds * 4 * 4 > 160 * 1024) return HM_ERR_UNSUPPORTED;
@@ -652,33 +790,13 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     const uint32_t staged_lds =
         even(A.cw + kHalo + (L - 1) * (cntP + cntAB) + L * cntX + 2 * L);
     A.staged = A.pad && (size_t)staged_lds * 4 * kAddWavesPerBlock <= 160 * 1024;
-    if (const char *e = getenv("HM_ADD_STAGED")) A.staged = A.staged && atoi(e) != 0;
     A.chain_lds = A.staged ? staged_lds : even(2 * (A.cw + kHalo) + (L - 1) * cntP);
     A.max_prod_words = SC;
     if ((size_t)A.chain_lds * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
-    if (const char *dbg = getenv("HM_DEBUG_SKIP")) A.debug_skip = (uint32_t)atoi(dbg);
-    // fused (one kernel, no workspace): staged chain whose inputs fit in the carry buffer.  Opt-in
-    // (HM_ADD_FUSED=1): measured 0.88 ms vs 0.81 ms per 4096 adds for prep + chain, because the
-    // 4 waves/SIMD of the chain grid all run their product prologue at once
-    const char *fz = getenv("HM_ADD_FUSED");
-    A.fused = fz && atoi(fz) != 0 && A.staged && (uint64_t)L * (cntA + cntB + 2) <= A.cw;
-    if (A.fused) {
-        A.a = batch_arg(a), A.b = batch_arg(b), A.out = batch_arg(out);
-        A.n = a->n, A.nbits = L;
-        A.status = c->d_status;
-        fill_bounds(A.ab, a), fill_bounds(A.bb, b), fill_bounds(A.ob, out);
-        DeviceGuard g(c->device);
-        return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
-    }
     A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
     const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
     DeviceGuard g(c->device);
-    if (bytes > c->ws_add_bytes) {
-        HM_HIP(c, hipStreamSynchronize(c->stream));
-        if (c->d_ws_add) (void)hipFree(c->d_ws_add), c->d_ws_add = nullptr, c->ws_add_bytes = 0;
-        HM_HIP(c, hipMalloc(&c->d_ws_add, bytes));
-        c->ws_add_bytes = bytes;
-    }
+    HM_HIP(c, grow(c, c->d_ws_add, c->ws_add_bytes, bytes));
     A.ws = c->d_ws_add;
     A.a = batch_arg(a), A.b = batch_arg(b), A.out = batch_arg(out);
     A.n = a->n, A.nbits = L;
@@ -718,12 +836,7 @@ static hm_status mul_impl(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint3
     M.lds_ints = 2 * L + 2 * P.kmax + 2;
     const size_t bytes = (size_t)o * 4 * a->n;
     DeviceGuard g(c->device);
-    if (bytes > c->ws_bytes) {
-        HM_HIP(c, hipStreamSynchronize(c->stream));
-        if (c->d_ws) (void)hipFree(c->d_ws), c->d_ws = nullptr, c->ws_bytes = 0;
-        HM_HIP(c, hipMalloc(&c->d_ws, bytes));
-        c->ws_bytes = bytes;
-    }
+    HM_HIP(c, grow(c, c->d_ws, c->ws_bytes, bytes));
     M.ws = c->d_ws;
     M.a = batch_arg(a), M.b = batch_arg(b), M.out = batch_arg(out);
     M.n = a->n, M.nbits = L, M.is_signed = is_signed;
@@ -836,12 +949,9 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
     if (ds == 0) return HM_ERR_DIVISOR_IS_ONE;       // the reference never terminates
     const size_t sl = ds / 64 + 1;
     DeviceGuard g(c->device);
-    if (c->d_s_limbs < sl) {
-        HM_HIP(c, hipStreamSynchronize(c->stream));
-        if (c->d_s) (void)hipFree(c->d_s);
-        HM_HIP(c, hipMalloc(&c->d_s, sl * 8));
-        c->d_s_limbs = sl;
-    }
+    size_t have = c->d_s_limbs * 8;
+    HM_HIP(c, grow(c, c->d_s, have, sl * 8));
+    c->d_s_limbs = have / 8;
     HM_HIP(c, hipMemcpyAsync(c->d_s, s, sl * 8, hipMemcpyHostToDevice, c->stream));
     HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer may be released after return
     return launch_poly_rem(poly_args(c, a, nullptr, out), c->d_s, (uint32_t)ds, c->stream)

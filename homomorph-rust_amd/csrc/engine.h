@@ -40,8 +40,6 @@ struct AddArgs {
     uint32_t cw;                      // chain: carry buffer words
     uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
     uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)
-    uint32_t fused;                   // one kernel: products computed into the staged LDS layout
-    uint32_t debug_skip;              // timing experiments only (HM_DEBUG_SKIP): 1 prep, 2 chain product
     int *status;
     Bounds ab, bb, ob;
 };
@@ -120,7 +118,17 @@ struct PolyArgs {
     int *status;
 };
 
+// Device CSPRNG: ChaCha20 (20 rounds, 256-bit key, 64-bit block counter, 64-bit nonce read from
+// *nonce and advanced by one per draw).  Block b of the draw fills bytes [64b, 64b + 64).
+struct RandArgs {
+    uint32_t key[8];
+    uint64_t *nonce;
+    uint8_t *out;
+    uint64_t nbytes;
+};
+
 // host-side launchers (kernels.hip)
+int launch_random(const RandArgs &a, void *stream);
 int launch_add(const AddArgs &a, void *stream);
 int launch_encrypt(const EncArgs &a, void *stream);
 int launch_decrypt(const DecArgs &a, void *stream);

@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
     // products only for bits < L-1 (the last bit has no outgoing carry)
-    const uint32_t nprod = (A.debug_skip & 1u) ? 0u : min(nmine, (L - 1) - min(i0, L - 1));
+    const uint32_t nprod = min(nmine, (L - 1) - min(i0, L - 1));
 
     // x_i = a_i ^ b_i for every bit: LDS for the P products, workspace for the chain's sum bits
     for (uint32_t f = lane; f < nmine * A.cntX; f += kWave) {
@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
     for (uint32_t i = 0; i < L; ++i) {
         store_sum_bit(pa + offa, rfl(da[i]), pb + offb, rfl(db[i]), C, nc, po + offo, A.ob.b[i],
                       dout + i, A.status);
-        if (i + 1 < L && !(A.debug_skip & 2u)) {
+        if (i + 1 < L) {
             const int np = bitwords((int)degPg[i]), nab = bitwords((int)degABg[i]);
             int nout;
             nc = words_of(wave_mul<kQBig, WMAX, PAD>(Pl + (size_t)i * A.cntP, np, C, nc,
@@ -506,99 +506,6 @@ __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
     for (uint32_t i = 0; i < L; ++i) {
         store_sum_x(Xl + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
                     A.status);
-        if (i + 1 < L && !(A.debug_skip & 2u)) {
-            const int np = bitwords((int)rfl(dPl[i])), nab = bitwords((int)rfl(dABl[i]));
-            int nout;
-            wsync(); // the sum bit's reads of C precede the in-place product's writes
-            nc = words_of(wave_mul<kQBig, WMAX, true>(Pl + (size_t)i * A.cntP, np, C, nc,
-                                                      ABl + (size_t)i * A.cntAB, nab, C, &nout));
-            wsync();
-        }
-        offo += cap_of(A.ob.b[i]);
-    }
-}
-
-// One kernel per add batch: each wavefront computes its value's carry-independent products
-// (x_i, ab_i, P_i, as add_prep_kernel does with several waves) straight into the staged LDS
-// layout, then runs the staged carry chain.  No workspace round trip through HBM and one launch;
-// the products' VALU work fills issue slots the chain's scalar branches leave idle on the SIMD.
-// The inputs are staged in the (not yet used) carry buffer, so LDS per wave equals the staged
-// chain's.
-template <int WMAX>
-__global__ void __launch_bounds__(256) add_fused_kernel(AddArgs A) {
-    extern __shared__ uint32_t lds[];
-    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
-    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (e >= A.n) return; // whole wave exits together
-    const int lane = lane_id();
-    const uint32_t L = A.nbits;
-    // LDS: [halo][C: cw][P: (L-1) cntP][AB: (L-1) cntAB][X: L cntX][degP+1: L][degAB+1: L]
-    uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
-    uint32_t *C = Ls + kHalo;
-    uint32_t *Pl = C + A.cw, *ABl = Pl + (size_t)(L - 1) * A.cntP;
-    uint32_t *Xl = ABl + (size_t)(L - 1) * A.cntAB, *dPl = Xl + (size_t)L * A.cntX, *dABl = dPl + L;
-    // inputs inside the carry buffer: [a: L cntA][b: L cntB][na: L][nb: L]
-    uint32_t *Al = C, *Bl = Al + (size_t)L * A.cntA, *nAl = Bl + (size_t)L * A.cntB, *nBl = nAl + L;
-    uint64_t *po = A.out.limbs + e * A.out.stride;
-    uint32_t *dout = A.out.degree + e * L;
-
-    stage_bits(A.a.limbs + e * A.a.stride, A.a.degree + e * L, A.ab, 0, L, Al, A.cntA, nAl, A.status);
-    stage_bits(A.b.limbs + e * A.b.stride, A.b.degree + e * L, A.bb, 0, L, Bl, A.cntB, nBl, A.status);
-    const uint32_t nprod = L - 1; // the last bit has no outgoing carry
-    for (uint32_t k = lane; k < 2 * L; k += kWave) dPl[k] = 0u; // dPl, dABl
-    for (uint32_t k = lane; k < nprod * A.cntAB; k += kWave) ABl[k] = 0u;
-    for (uint32_t k = lane; k < nprod * A.cntP; k += kWave) Pl[k] = 0u;
-    wsync();
-    // x_i = a_i ^ b_i, every bit
-    for (uint32_t f = lane; f < L * A.cntX; f += kWave) {
-        const uint32_t t = f / A.cntX, m = f % A.cntX;
-        const int na = (int)nAl[t], nb = (int)nBl[t];
-        Xl[f] = ((int)m < na ? Al[t * A.cntA + m] : 0u) ^ ((int)m < nb ? Bl[t * A.cntB + m] : 0u);
-    }
-    // products by rows, lanes over (bit t, multiplier word q); rows meet in LDS through ds_xor
-    const uint32_t cq = A.cntX;
-    auto for_rows = [&](auto &&row) {
-        const uint32_t dt = kWave / cq, dq = kWave % cq;
-        uint32_t t = (uint32_t)lane / cq, q = (uint32_t)lane % cq;
-        for (uint32_t f0 = 0; f0 < nprod * cq; f0 += kWave) {
-            if (t < nprod) row(t, q);
-            t += dt, q += dq;
-            if (q >= cq) q -= cq, ++t;
-        }
-    };
-    wsync();
-    for_rows([&](uint32_t t, uint32_t q) { // ab_i = a_i * b_i
-        if ((int)q < (int)nAl[t])
-            clmul_row_xor(Al[t * A.cntA + q], Bl + t * A.cntB, (int)nBl[t], ABl + t * A.cntAB + q);
-    });
-    wsync();
-    for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
-        const uint32_t w = ABl[f];
-        if (w) atomicMax(&dABl[f / A.cntAB], (f % A.cntAB) * 32 + 32 - __builtin_clz(w));
-    }
-    wsync();
-    for_rows([&](uint32_t t, uint32_t q) { // x_i * ab_i
-        const int nx = max((int)nAl[t], (int)nBl[t]);
-        if ((int)q < nx)
-            clmul_row_xor(Xl[t * A.cntX + q], ABl + t * A.cntAB, bitwords((int)dABl[t]),
-                          Pl + t * A.cntP + q);
-    });
-    wsync();
-    for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) { // P_i = x_i ^ x_i * ab_i
-        const uint32_t t = f / A.cntP, m = f % A.cntP;
-        const uint32_t w = Pl[f] ^ (m < A.cntX ? Xl[t * A.cntX + m] : 0u);
-        Pl[f] = w;
-        if (w) atomicMax(&dPl[t], m * 32 + 32 - __builtin_clz(w));
-    }
-    // the inputs are consumed: clear the carry buffer and its halo
-    for (uint32_t k = lane; k < kHalo + A.cw; k += kWave) Ls[k] = 0u;
-    wsync();
-
-    int nc = 0; // carry words (0 = null carry, common.rs:39)
-    uint32_t offo = 0;
-    for (uint32_t i = 0; i < L; ++i) {
-        store_sum_x(Xl + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
-                    A.status);
         if (i + 1 < L) {
             const int np = bitwords((int)rfl(dPl[i])), nab = bitwords((int)rfl(dABl[i]));
             int nout;
@@ -613,21 +520,6 @@ __global__ void __launch_bounds__(256) add_fused_kernel(AddArgs A) {
 
 int launch_add(const AddArgs &a, void *stream) {
     if (a.n == 0) return 0;
-    if (a.fused) {
-        const uint64_t blocks = (a.n + kAddWavesPerBlock - 1) / kAddWavesPerBlock;
-        const size_t lds = (size_t)a.chain_lds * 4 * kAddWavesPerBlock;
-        const uint32_t need = (a.max_prod_words + 63) / 64;
-#define HM_LAUNCH_FUSED(WM)                                                                       \
-    hipLaunchKernelGGL((add_fused_kernel<WM>), dim3((unsigned)blocks), dim3(64 * kAddWavesPerBlock), \
-                       lds, (hipStream_t)stream, a)
-        if (need <= 4) HM_LAUNCH_FUSED(4);
-        else if (need <= 8) HM_LAUNCH_FUSED(8);
-        else if (need <= 12) HM_LAUNCH_FUSED(12);
-        else if (need <= 16) HM_LAUNCH_FUSED(16);
-        else HM_LAUNCH_FUSED(24);
-#undef HM_LAUNCH_FUSED
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
     // prep: wpv waves per value, 4 waves per block
     {
         const uint64_t waves = a.n * a.wpv;
@@ -1016,7 +908,7 @@ static void launch_enc_pc(const EncArgs &E, void *stream) {
     const uint64_t threads = E.n * E.nbytes * 8;
     const size_t tab = (size_t)((E.tau + 3) / 4) * ((PC + 1) / 2) * 16 * 16;
     const size_t lds = tab + (size_t)kEncBlock * PC * 8; // + the store transpose
-    if (E.pk_tab && tab <= kEncTableBytes && lds <= 64 * 1024 && !getenv("HM_ENC_PLAIN")) {
+    if (E.pk_tab && tab <= kEncTableBytes && lds <= 64 * 1024) {
         // a few resident blocks per CU, each striding over bits (the table copy is amortised)
         const uint64_t want = (threads + kEncBlock - 1) / kEncBlock;
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
@@ -1150,16 +1042,76 @@ __global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
 
 int launch_decrypt(const DecArgs &D, void *stream) {
     if (D.n == 0) return 0;
-    if (D.maxcap <= 32 && !getenv("HM_DEC_WAVE")) {
+    if (D.maxcap <= 32) {
         const uint64_t blocks = (D.n * D.nbits + 255) / 256;
         hipLaunchKernelGGL(decrypt_bits_kernel, dim3((unsigned)blocks), dim3(256), 0,
                            (hipStream_t)stream, D);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    const char *env = getenv("HM_DEC_WPB");
-    const uint32_t wpb = env ? (uint32_t)atoi(env) : 4u;
+    const uint32_t wpb = 4u;
     const uint64_t blocks = (D.n + wpb - 1) / wpb;
     hipLaunchKernelGGL(decrypt_kernel, dim3((unsigned)blocks), dim3(64 * wpb), 0, (hipStream_t)stream, D);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Device CSPRNG for encryption masks: ChaCha20 (D. J. Bernstein's original layout: constants,
+// 256-bit key, 64-bit block counter, 64-bit nonce), one 64-byte block per thread.  The nonce is
+// read from device memory and advanced by rand_bump_kernel after the draw, so a graph replay
+// never repeats a keystream.
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
+
+#define HM_QR(a, b, c, d)                                                                          \
+    a += b, d = rotl32(d ^ a, 16), c += d, b = rotl32(b ^ c, 12), a += b, d = rotl32(d ^ a, 8),   \
+    c += d, b = rotl32(b ^ c, 7)
+
+__global__ void __launch_bounds__(256) rand_fill_kernel(RandArgs R) {
+    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blk * 64 >= R.nbytes) return;
+    const uint64_t nonce = *R.nonce;
+    uint32_t x[16], s[16];
+    s[0] = 0x61707865u, s[1] = 0x3320646eu, s[2] = 0x79622d32u, s[3] = 0x6b206574u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[4 + i] = R.key[i];
+    s[12] = (uint32_t)blk, s[13] = (uint32_t)(blk >> 32);
+    s[14] = (uint32_t)nonce, s[15] = (uint32_t)(nonce >> 32);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = s[i];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        HM_QR(x[0], x[4], x[8], x[12]);
+        HM_QR(x[1], x[5], x[9], x[13]);
+        HM_QR(x[2], x[6], x[10], x[14]);
+        HM_QR(x[3], x[7], x[11], x[15]);
+        HM_QR(x[0], x[5], x[10], x[15]);
+        HM_QR(x[1], x[6], x[11], x[12]);
+        HM_QR(x[2], x[7], x[8], x[13]);
+        HM_QR(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] += s[i];
+    uint8_t *dst = R.out + blk * 64;
+    if (blk * 64 + 64 <= R.nbytes && ((uintptr_t)dst & 15u) == 0) {
+        uint4 *d4 = (uint4 *)dst;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d4[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+    } else {
+        for (uint64_t k = 0; k < 64 && blk * 64 + k < R.nbytes; ++k)
+            dst[k] = (uint8_t)(x[k / 4] >> (8 * (k % 4)));
+    }
+}
+#undef HM_QR
+
+__global__ void rand_bump_kernel(uint64_t *nonce) {
+    if (threadIdx.x == 0) atomicAdd((unsigned long long *)nonce, 1ull);
+}
+
+int launch_random(const RandArgs &R, void *stream) {
+    if (!R.nbytes) return 0;
+    const uint64_t blocks = (R.nbytes + 64 * 256 - 1) / (64 * 256);
+    hipLaunchKernelGGL(rand_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, R);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(rand_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, R.nonce);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

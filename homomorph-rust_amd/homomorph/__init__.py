@@ -30,6 +30,7 @@ __all__ = [
     "HomomorphicAndGate", "HomomorphicOrGate", "HomomorphicXorGate", "HomomorphicNotGate",
     "HomomorphicAddition", "HomomorphicMultiplication",
     "OperationError", "ContextCryptoError", "CipherError", "EngineError", "LibraryMissing",
+    "EngineGraph",
     "add_out_bounds", "mul_out_bounds", "gate_out_bounds", "batch_stride", "caps",
 ]
 
@@ -67,7 +68,7 @@ def _check(st: int, what: str):
         return
     if st in (_lib.ERR_SECRET_KEY_UNSET, _lib.ERR_PUBLIC_KEY_UNSET):
         raise ContextCryptoError(st, what)
-    if st == _lib.ERR_INVALID_CIPHERED_LENGTH:
+    if st in (_lib.ERR_INVALID_CIPHERED_LENGTH, _lib.ERR_RANDOMNESS):
         raise CipherError(st, what)
     if st == _lib.ERR_DIVIDE_BY_ZERO:
         raise ZeroDivisionError("attempt to divide by zero")  # polynomial.rs:319-322
@@ -362,20 +363,45 @@ class Context:
         cur.wait_stream(self._stream)
         _check(st, what)
 
-    def graph(self, fn, warmup: int = 1):
+    def graph(self, fn, warmup: int = 1) -> "EngineGraph":
         """Capture the engine launches `fn` makes into one HIP graph on the engine stream and
-        return it (a torch.cuda.CUDAGraph; `.replay()` re-runs it on the current stream, over the
-        same buffers).  `fn` runs `warmup` times first, so that workspaces and decrypt tables are
-        allocated outside the capture; launch-bound sequences (encrypt + decrypt of a batch) then
-        cost one graph launch instead of one host round trip per kernel."""
+        return it (`.replay()` re-runs it over the same buffers).  `fn` runs `warmup` times
+        first, so that workspaces and decrypt tables are allocated outside the capture;
+        launch-bound sequences (encrypt + decrypt of a batch) then cost one graph launch instead
+        of one host round trip per kernel.  The graph holds raw pointers to the context's
+        buffers: it refuses to replay once the context has replaced any of them
+        (hm_ctx_generation, e.g. after a bigger batch or a new key)."""
         torch = _torch()
         for _ in range(warmup):
             fn()
         self.synchronize()
+        gen = self.generation()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self._stream):
             fn()
-        return g
+        if self.generation() != gen:
+            raise EngineError(_lib.ERR_INVALID_ARGUMENT,
+                              "graph capture: the context replaced a buffer during capture "
+                              "(run more warm-up calls)")
+        return EngineGraph(self, g, gen)
+
+    def generation(self) -> int:
+        return int(lib().hm_ctx_generation(self._h))
+
+    def trim(self):
+        """Free retired device buffers (no graph captured earlier may be replayed after)."""
+        _check(lib().hm_ctx_trim(self._h), "hm_ctx_trim")
+
+    def mask_bytes(self) -> int:
+        """Mask bytes per ciphertext bit: ceil(tau/8) for the LOADED public key's tau."""
+        return int(lib().hm_ctx_mask_bytes(self._h))
+
+    def random_bytes(self, n: int):
+        """n bytes of the context's device CSPRNG (ChaCha20) as a uint8 device tensor."""
+        torch = _torch()
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self._launch(lambda: lib().hm_random_bytes(self._h, out.data_ptr(), n), "random_bytes")
+        return out
 
     @property
     def stream(self):
@@ -429,11 +455,12 @@ class Context:
         return PublicKey(out)
 
     # ---- cipher
-    def encrypt(self, data, masks=None, generator=None, bound=None) -> Ciphered:
+    def encrypt(self, data, masks=None, bound=None) -> Ciphered:
         """Context::encrypt over a batch.  data: 1-D array of one integer dtype (the bincode fixint
         LE image of each value is its little-endian bytes) or an (n, nbytes) uint8 array.  masks:
-        (n, 8*nbytes, ceil(tau/8)) uint8 subset masks (the bytes CipheredBit::part draws,
-        cipher.rs:92-97); drawn on the device when omitted."""
+        (n, 8*nbytes, ceil(tau/8)) uint8 subset masks with tau = the loaded public key's row count
+        (the bytes CipheredBit::part draws, cipher.rs:92-97) -- the parity-test contract; when
+        omitted the engine draws them from its CSPRNG, as the reference draws from getrandom."""
         torch = _torch()
         plain_dtype = None
         if isinstance(data, torch.Tensor):
@@ -447,24 +474,26 @@ class Context:
             raw = raw.reshape(arr.shape[0], arr.dtype.itemsize)
         n, nbytes = raw.shape
         nbits = 8 * nbytes
-        mb = (self._params.tau + 7) // 8
+        mb = self.mask_bytes()
+        if mb == 0:
+            _check(_lib.ERR_PUBLIC_KEY_UNSET, "encrypt")
         dev_data = torch.from_numpy(raw).to(self.device)
         if masks is None:
-            dev_masks = torch.randint(0, 256, (n, nbits, mb), dtype=torch.uint8,
-                                      device=self.device, generator=generator)
+            dev_masks = None
         elif isinstance(masks, torch.Tensor):
             dev_masks = masks.to(self.device, torch.uint8).contiguous()
         else:
             dev_masks = torch.from_numpy(np.ascontiguousarray(masks, dtype=np.uint8)).to(self.device)
-        if dev_masks.numel() != n * nbits * mb:
-            raise ValueError("masks must be (n, 8*nbytes, ceil(tau/8)) bytes")
+        if dev_masks is not None and dev_masks.numel() != n * nbits * mb:
+            raise ValueError(f"masks must be (n, 8*nbytes, {mb}) bytes: ceil(tau/8) per bit for "
+                             f"the loaded public key's tau")
         if bound is None:
             bound = np.full(nbits, self.fresh_bound(), dtype=np.uint32)
         out = Ciphered.empty(n, bound, self.device, plain_dtype)
         c = out._c()
-        self._launch(lambda: lib().hm_encrypt_batch(self._h, dev_data.data_ptr(), nbytes,
-                                                    dev_masks.data_ptr(), ctypes.byref(c)),
-                     "encrypt")
+        mptr = None if dev_masks is None else dev_masks.data_ptr()
+        self._launch(lambda: lib().hm_encrypt_batch(self._h, dev_data.data_ptr(), nbytes, mptr,
+                                                    ctypes.byref(c)), "encrypt")
         out._keep = (dev_data, dev_masks)
         return out
 
@@ -571,6 +600,21 @@ class Context:
         """Wait for the engine's stream; raise the first device-side error flagged since the
         last check (capacity / bad input)."""
         _check(lib().hm_ctx_synchronize(self._h), "device")
+
+
+class EngineGraph:
+    """A captured sequence of engine launches (Context.graph).  Replays only while the context
+    still owns the buffers the capture recorded (hm_ctx_generation unchanged)."""
+
+    def __init__(self, ctx: Context, graph, generation: int):
+        self._ctx, self._g, self._gen = ctx, graph, generation
+
+    def replay(self):
+        if self._ctx.generation() != self._gen:
+            raise EngineError(_lib.ERR_INVALID_ARGUMENT,
+                              "graph replay: the context replaced a buffer this graph uses "
+                              "(capture it again)")
+        self._g.replay()
 
 
 def add_into(ctx: Context, a: Ciphered, b: Ciphered, out: Ciphered) -> None:

@@ -27,6 +27,7 @@ ERR_HIP = 8
 ERR_INVALID_ARGUMENT = 9
 ERR_INVALID_CIPHERED_LENGTH = 10
 ERR_BAD_INPUT = 11
+ERR_RANDOMNESS = 12
 
 # hm_op
 OP_AND, OP_OR, OP_XOR, OP_NOT, OP_ADD, OP_MUL, OP_MUL_SIGNED = range(7)
@@ -53,6 +54,10 @@ SIGNATURES = {
     "hm_abi_version": (ctypes.c_uint32, []),
     "hm_ctx_create": (ctypes.c_int, [ctypes.c_uint16] * 4 + [ctypes.c_int, ctypes.POINTER(vp)]),
     "hm_ctx_destroy": (None, [vp]),
+    "hm_ctx_generation": (ctypes.c_uint64, [vp]),
+    "hm_ctx_trim": (ctypes.c_int, [vp]),
+    "hm_ctx_mask_bytes": (ctypes.c_uint32, [vp]),
+    "hm_random_bytes": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
     "hm_ctx_set_stream": (ctypes.c_int, [vp, vp]),
     "hm_ctx_stream": (vp, [vp]),
     "hm_ctx_parameters": (ctypes.c_int, [vp, u16p, u16p, u16p, u16p]),

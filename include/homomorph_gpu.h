@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 1
+#define HM_ABI_VERSION 2
 #define HM_MAX_BITS 128 /* u128 is the widest type with impls (src/impls/numbers/uint.rs:58) */
 
 typedef enum hm_status {
@@ -58,6 +58,8 @@ typedef enum hm_status {
     HM_ERR_INVALID_CIPHERED_LENGTH = 10,
     /* an input polynomial's degree word disagrees with its limbs (device-side check) */
     HM_ERR_BAD_INPUT = 11,
+    /* CipherError::Randomness (src/cipher.rs:18-24): the OS random source failed */
+    HM_ERR_RANDOMNESS = 12,
 } hm_status;
 
 /* Operation marker types and their OperationRequirement::MIN_D_OVER_DELTA
@@ -103,6 +105,14 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
 /* Drop: device copies of the secret key (and tables derived from it) are zeroed before release,
  * mirroring SecretKey's Drop (src/context.rs:197-206). */
 void hm_ctx_destroy(hm_ctx *ctx);
+/* Device buffers the kernels read (workspaces, key tables, decrypt tables, mask buffers) are
+ * never freed while the context lives, because a HIP graph captured over the engine's launches
+ * holds their raw pointers.  When one must be replaced (it grows, or a new key replaces its
+ * contents) the old one is retired -- zeroed first if it holds secret-derived data -- and the
+ * context generation advances.  A captured graph is valid only while the generation it was
+ * captured at is current; hm_ctx_trim frees the retired buffers (no graph may use them after). */
+uint64_t hm_ctx_generation(const hm_ctx *ctx);
+hm_status hm_ctx_trim(hm_ctx *ctx);
 /* Launch on a caller stream (hipStream_t passed as void*; NULL = the default null stream, as in
  * HIP) instead of the context's own non-blocking stream.  Use it to order the engine's launches
  * with the caller's copies, e.g. torch.cuda.current_stream().cuda_stream. */
@@ -121,11 +131,14 @@ hm_status hm_ctx_set_secret_key(hm_ctx *ctx, const uint64_t *limbs, size_t nlimb
 hm_status hm_ctx_set_public_key(hm_ctx *ctx, const uint64_t *limbs, uint32_t tau,
                                 uint32_t limbs_per_poly);
 /* Context::generate_secret_key / generate_public_key — src/context.rs:421-454 (keygen shape
- * S = random(d), T_i = S*Q_i + X*R_i, :160-162 and :249-261).  The reference draws from
- * getrandom; here both draw from the context's SplitMix64 stream (DESIGN.md "RNG contract"),
- * seeded from the OS at creation or explicitly with hm_ctx_seed_rng for reproducible keys.
+ * S = random(d), T_i = S*Q_i + X*R_i, :160-162 and :249-261).  As in the reference, every key
+ * polynomial is drawn from getrandom(2) (src/polynomial.rs:73-96) and encryption masks from a
+ * CSPRNG (a device ChaCha20 stream keyed with 32 getrandom bytes at context creation).
+ * hm_ctx_seed_rng is a TEST hook: it switches key generation to a SplitMix64 stream and the mask
+ * stream to a ChaCha20 key derived from the seed, so parity tests can reproduce both sides.
  * generate_secret_key clears the public key (:421-424); generate_public_key needs the secret key
- * (HM_ERR_SECRET_KEY_UNSET otherwise, :444-454). */
+ * (HM_ERR_SECRET_KEY_UNSET otherwise, :444-454).  Public-key rows are as wide as the widest
+ * T_i (deg S + dp for a loaded secret key of any degree). */
 hm_status hm_ctx_seed_rng(hm_ctx *ctx, uint64_t seed);
 hm_status hm_ctx_generate_secret_key(hm_ctx *ctx);
 hm_status hm_ctx_generate_public_key(hm_ctx *ctx);
@@ -138,8 +151,13 @@ hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
  * the OperationError payload written to *required_min_d_over_delta (may be NULL). */
 hm_status hm_validate_operation(const hm_ctx *ctx, hm_op op, uint16_t *required_min_d_over_delta);
 
-/* Static degree bounds (host only, no device work).  fresh bound = d + dp. */
+/* Static degree bounds (host only, no device work).  fresh bound = max(d + dp, max deg T_i):
+ * a subset sum of public-key rows plus the plaintext bit (cipher.rs:99-115). */
 uint32_t hm_fresh_bound(const hm_ctx *ctx);
+/* Mask bytes per ciphertext bit: ceil(tau/8) with tau = the number of rows of the LOADED public
+ * key (CipheredBit::cipher takes tau = pk.len(), cipher.rs:101-103; a loaded key may differ from
+ * Parameters::tau, context.rs:585-593).  0 when no public key is set. */
+uint32_t hm_ctx_mask_bytes(const hm_ctx *ctx);
 /* Output bounds of the ripple-carry adder (common.rs:37-56) for input bounds a,b (nbits each). */
 hm_status hm_add_out_bounds(uint32_t nbits, const uint32_t *a_bound, const uint32_t *b_bound,
                             uint32_t *out_bound);
@@ -153,12 +171,17 @@ hm_status hm_gate_out_bounds(hm_op gate, uint32_t nbits, const uint32_t *a_bound
 uint64_t hm_batch_stride(uint32_t nbits, const uint32_t *bound);
 
 /* ---------------- cipher (src/cipher.rs) ---------------- */
+/* n bytes of the context's mask CSPRNG (device ChaCha20, see hm_ctx_seed_rng) into device
+ * memory.  Every call -- and every replay of a graph that captured one -- draws fresh bytes. */
+hm_status hm_random_bytes(hm_ctx *ctx, uint8_t *dev_dst, size_t nbytes);
 /* Context::encrypt over a batch — Ciphered::try_cipher (cipher.rs:175-191) and
  * CipheredBit::cipher (:99-115).  data: device, n*nbytes plaintext bytes (the bincode fixint LE
- * image of each value).  masks: device, n*(8*nbytes)*ceil(tau/8) bytes; bit k of value e uses the
- * ceil(tau/8) bytes at ((e*8*nbytes)+k)*ceil(tau/8), mask bit i = byte[i/8] >> (i%8) & 1 — exactly
- * the bytes CipheredBit::part (:92-97) draws from getrandom.  out: nbits = 8*nbytes, every bound
- * >= hm_fresh_bound.  Requires the public key. */
+ * image of each value).  masks: NULL = the engine draws them from its CSPRNG, as
+ * CipheredBit::part (:92-97) draws from getrandom (the default); or device,
+ * n*(8*nbytes)*M bytes with M = hm_ctx_mask_bytes(ctx): bit k of value e uses the M bytes at
+ * ((e*8*nbytes)+k)*M, mask bit i = byte[i/8] >> (i%8) & 1 — exactly the bytes part() draws (the
+ * test contract).  out: nbits = 8*nbytes, every bound >= hm_fresh_bound.  Requires the public
+ * key. */
 hm_status hm_encrypt_batch(hm_ctx *ctx, const uint8_t *data, uint32_t nbytes,
                            const uint8_t *masks, hm_batch *out);
 /* Context::decrypt over a batch — Ciphered::try_decipher (cipher.rs:217-250): bit k =

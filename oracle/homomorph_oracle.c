@@ -23,7 +23,7 @@ typedef struct {
     size_t deg;
 } poly;
 
-static uint64_t g_limb_products = 0;
+static _Thread_local uint64_t g_limb_products = 0; /* calling thread only */
 uint64_t oracle_limb_products(void) { return g_limb_products; }
 void oracle_reset_counters(void) { g_limb_products = 0; }
 
@@ -473,6 +473,37 @@ static void mul_internal(const poly *a, const poly *b, uint32_t L, int is_signed
 
 typedef enum { K_ADD, K_MUL, K_MULS, K_AND, K_OR, K_XOR, K_NOT } kind;
 
+static int g_threads = 1; /* oracle_set_threads: batch-parallel CPU baseline (bench.py) */
+
+void oracle_set_threads(int n) { g_threads = n > 0 ? n : 1; }
+
+/* One value of a binary circuit (the reference runs one value per call, single-threaded). */
+static int run_one(kind k, const uint64_t *a, const uint32_t *adeg, const uint32_t *abound,
+                   const uint64_t *b, const uint32_t *bdeg, const uint32_t *bbound,
+                   uint32_t nbits, size_t e, uint64_t *out, uint32_t *odeg,
+                   const uint32_t *obound, const size_t *offa, size_t sa, const size_t *offb,
+                   size_t sb, const size_t *offo, size_t so, poly *pa, poly *pb, poly *pr) {
+    int st = load_bits(a, adeg, abound, nbits, e, offa, sa, pa);
+    if (st) return st;
+    st = load_bits(b, bdeg, bbound, nbits, e, offb, sb, pb);
+    if (st) {
+        for (uint32_t i = 0; i < nbits; i++) p_free(&pa[i]);
+        return st;
+    }
+    switch (k) {
+    case K_ADD: add_internal(pa, pb, nbits, pr); break;
+    case K_MUL: mul_internal(pa, pb, nbits, 0, pr); break;
+    case K_MULS: mul_internal(pa, pb, nbits, 1, pr); break;
+    case K_AND: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_and(&pa[i], &pb[i]); break;
+    case K_OR: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_or(&pa[i], &pb[i]); break;
+    case K_XOR: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_xor(&pa[i], &pb[i]); break;
+    case K_NOT: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_not(&pa[i]); break;
+    }
+    st = store_bits(pr, nbits, e, out, odeg, obound, offo, so);
+    for (uint32_t i = 0; i < nbits; i++) p_free(&pa[i]), p_free(&pb[i]), p_free(&pr[i]);
+    return st;
+}
+
 static int run_binary(kind k, const uint64_t *a, const uint32_t *adeg, const uint32_t *abound,
                       const uint64_t *b, const uint32_t *bdeg, const uint32_t *bbound,
                       uint32_t nbits, size_t n, uint64_t *out, uint32_t *odeg,
@@ -482,31 +513,25 @@ static int run_binary(kind k, const uint64_t *a, const uint32_t *adeg, const uin
     size_t *offo = (size_t *)xcalloc(nbits, sizeof(size_t));
     size_t sa = layout(abound, nbits, offa), sb = layout(bbound, nbits, offb);
     size_t so = layout(obound, nbits, offo);
-    poly *pa = (poly *)xcalloc(nbits, sizeof(poly));
-    poly *pb = (poly *)xcalloc(nbits, sizeof(poly));
-    poly *pr = (poly *)xcalloc(nbits, sizeof(poly));
     int st = OR_OK;
-    for (size_t e = 0; e < n && st == OR_OK; e++) {
-        st = load_bits(a, adeg, abound, nbits, e, offa, sa, pa);
-        if (st) break;
-        st = load_bits(b, bdeg, bbound, nbits, e, offb, sb, pb);
-        if (st) {
-            for (uint32_t i = 0; i < nbits; i++) p_free(&pa[i]);
-            break;
+    /* values are independent: the all-cores baseline splits the batch over threads */
+#pragma omp parallel num_threads(g_threads) if (g_threads > 1 && n > 1)
+    {
+        poly *pa = (poly *)xcalloc(nbits, sizeof(poly));
+        poly *pb = (poly *)xcalloc(nbits, sizeof(poly));
+        poly *pr = (poly *)xcalloc(nbits, sizeof(poly));
+#pragma omp for schedule(dynamic, 1)
+        for (size_t e = 0; e < n; e++) {
+            int r = run_one(k, a, adeg, abound, b, bdeg, bbound, nbits, e, out, odeg, obound,
+                            offa, sa, offb, sb, offo, so, pa, pb, pr);
+            if (r) {
+#pragma omp critical
+                if (!st) st = r;
+            }
         }
-        switch (k) {
-        case K_ADD: add_internal(pa, pb, nbits, pr); break;
-        case K_MUL: mul_internal(pa, pb, nbits, 0, pr); break;
-        case K_MULS: mul_internal(pa, pb, nbits, 1, pr); break;
-        case K_AND: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_and(&pa[i], &pb[i]); break;
-        case K_OR: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_or(&pa[i], &pb[i]); break;
-        case K_XOR: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_xor(&pa[i], &pb[i]); break;
-        case K_NOT: for (uint32_t i = 0; i < nbits; i++) pr[i] = cb_not(&pa[i]); break;
-        }
-        st = store_bits(pr, nbits, e, out, odeg, obound, offo, so);
-        for (uint32_t i = 0; i < nbits; i++) p_free(&pa[i]), p_free(&pb[i]), p_free(&pr[i]);
+        free(pa), free(pb), free(pr);
     }
-    free(offa), free(offb), free(offo), free(pa), free(pb), free(pr);
+    free(offa), free(offb), free(offo);
     return st;
 }
 

@@ -87,7 +87,12 @@ int oracle_gate_batch(int op, const uint64_t *a, const uint32_t *adeg, const uin
                       uint32_t nbits, size_t n,
                       uint64_t *out, uint32_t *odeg, const uint32_t *obound);
 
-/* Work counter: 64x64 limb products issued by oracle_poly_mul since the last reset. */
+/* Threads for the batch entry points (values split over threads; default 1, the reference is
+ * single-threaded).  Used by bench.py's all-cores CPU baseline leg. */
+void oracle_set_threads(int n);
+
+/* Work counter: 64x64 limb products issued by oracle_poly_mul on the calling thread since the
+ * last reset. */
 uint64_t oracle_limb_products(void);
 void oracle_reset_counters(void);
 

@@ -60,6 +60,8 @@ def lib():
         L.oracle_mul_batch.argtypes = binargs + [ctypes.c_int, u64p, u32p, u32p]
         L.oracle_gate_batch.restype = ctypes.c_int
         L.oracle_gate_batch.argtypes = [ctypes.c_int] + binargs + [u64p, u32p, u32p]
+        L.oracle_set_threads.restype = None
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
         L.oracle_limb_products.restype = ctypes.c_uint64
         L.oracle_reset_counters.restype = None
         _lib = L
@@ -201,6 +203,12 @@ GATES = {"and": 0, "or": 1, "xor": 2, "not": 3}
 
 def gate_batch(op, a, adeg, abound, b, bdeg, bbound, nbits, n, obound):
     return _binary("gate", a, adeg, abound, b, bdeg, bbound, nbits, n, obound, GATES[op])
+
+
+def set_threads(n: int):
+    """Threads for the batch entry points (values split over threads); 1 = the reference's
+    single-threaded execution."""
+    lib().oracle_set_threads(int(n))
 
 
 def limb_products() -> int:

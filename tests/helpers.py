@@ -71,3 +71,54 @@ def low_bits(limbs, deg, bound, n, k):
     l = np.asarray(limbs, dtype=np.uint64).reshape(n, stride)[:, :sk].reshape(-1).copy()
     d = np.asarray(deg, dtype=np.uint32).reshape(n, len(bound))[:, :k].reshape(-1).copy()
     return l, d, np.ascontiguousarray(np.asarray(bound, dtype=np.uint32)[:k])
+
+
+# ------------------------------------------------------------------ mask CSPRNG contract
+def _splitmix64(state):
+    state = (state + 0x9E3779B97F4A7C15) & (2**64 - 1)
+    z = state
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+    return state, z ^ (z >> 31)
+
+
+def chacha20_block(key_words, counter, nonce):
+    """One 64-byte ChaCha20 block (Bernstein's layout: 64-bit counter, 64-bit nonce), pure
+    Python: the test-side restatement of the engine's mask generator (kernels.hip)."""
+    M = 0xFFFFFFFF
+
+    def rotl(x, r):
+        return ((x << r) | (x >> (32 - r))) & M
+
+    def qr(x, a, b, c, d):
+        x[a] = (x[a] + x[b]) & M; x[d] = rotl(x[d] ^ x[a], 16)
+        x[c] = (x[c] + x[d]) & M; x[b] = rotl(x[b] ^ x[c], 12)
+        x[a] = (x[a] + x[b]) & M; x[d] = rotl(x[d] ^ x[a], 8)
+        x[c] = (x[c] + x[d]) & M; x[b] = rotl(x[b] ^ x[c], 7)
+
+    s = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574] + list(key_words) + [
+        counter & M, counter >> 32, nonce & M, (nonce >> 32) & M]
+    x = list(s)
+    for _ in range(10):
+        qr(x, 0, 4, 8, 12); qr(x, 1, 5, 9, 13); qr(x, 2, 6, 10, 14); qr(x, 3, 7, 11, 15)
+        qr(x, 0, 5, 10, 15); qr(x, 1, 6, 11, 12); qr(x, 2, 7, 8, 13); qr(x, 3, 4, 9, 14)
+    return b"".join(((x[i] + s[i]) & M).to_bytes(4, "little") for i in range(16))
+
+
+def seeded_chacha(seed):
+    """(key words, first nonce) of a context after hm_ctx_seed_rng(seed) (capi.cpp)."""
+    st = seed ^ 0x6D61736B73636861
+    key = []
+    for _ in range(4):
+        st, w = _splitmix64(st)
+        key += [w & 0xFFFFFFFF, w >> 32]
+    st, nonce = _splitmix64(st)
+    return key, nonce
+
+
+def seeded_random_bytes(seed, draw, n):
+    """Bytes of the `draw`-th (0-based) hm_random_bytes call of size n after seeding."""
+    key, nonce = seeded_chacha(seed)
+    nonce = (nonce + draw) & (2**64 - 1)
+    blocks = [chacha20_block(key, c, nonce) for c in range((n + 63) // 64)]
+    return np.frombuffer(b"".join(blocks)[:n], dtype=np.uint8)

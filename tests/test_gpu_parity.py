@@ -187,28 +187,6 @@ def test_add_parity(H, oracle, params, dtype, n):
         assert np.array_equal(dec, (a + b).astype(dtype))
 
 
-@pytest.mark.parametrize("params,dtype,n", [((128, 128, 1, 128), np.uint32, 24),
-                                            ((64, 64, 1, 64), np.uint8, 64)])
-def test_add_fused_kernel_parity(H, oracle, params, dtype, n, monkeypatch):
-    """The opt-in one-kernel adder (HM_ADD_FUSED=1: products computed into the staged LDS
-    layout) against the oracle, like test_add_parity."""
-    monkeypatch.setenv("HM_ADD_FUSED", "1")
-    d, dp, delta, tau = params
-    ctx = make_ctx(H, params, 19)
-    sk, pk, _ = keys(*params, 19)
-    a, b, ma, mb, ca, cb = _pair(H, ctx, params, dtype, n, 20)
-    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
-    ctx.synchronize()
-    nbits = 8 * np.dtype(dtype).itemsize
-    bound = fresh_bound(d, dp, nbits)
-    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
-    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
-    ob = H.add_out_bounds(bound, bound)
-    rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, nbits, n, ob)
-    gl, gd = cs.to_host()
-    assert_batches_equal(gl, gd, rl, rd, ob, n, "fused add")
-
-
 def test_add_edge_values(H, oracle):
     """Wrap-around and extremes (uint.rs:202-208: 255 + 240 = 239), zero, all-ones."""
     params = (128, 128, 1, 128)
