@@ -15,78 +15,11 @@
 
 #include <sys/random.h>
 
-#include "engine.h"
-#include "gf2_wave.h"
+#include "ctx.h"
 
 using namespace hm;
 
-struct hm_ctx {
-    uint16_t d, dp, delta, tau;
-    int device;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    // Randomness.  Unseeded (the default): key polynomials come straight from getrandom(2), as
-    // Polynomial::random does (src/polynomial.rs:73-96), and encryption masks from a device
-    // ChaCha20 keystream keyed with 32 getrandom bytes.  hm_ctx_seed_rng switches both to a
-    // reproducible test contract: SplitMix64 for keys, a ChaCha20 key derived from the seed.
-    bool seeded = false;
-    uint64_t rng = 0;
-    uint32_t chacha_key[8] = {};
-    uint64_t *d_nonce = nullptr;       // device ChaCha20 nonce counter, advanced by every draw
-    // keys (host copies; SecretKey / PublicKey)
-    bool has_sk = false, has_pk = false;
-    std::vector<uint64_t> sk;          // limbs of S
-    std::vector<uint64_t> pk;          // tau * pk_cap limbs
-    uint32_t pk_tau = 0, pk_cap = 0;
-    uint32_t pk_maxdeg = 0;
-    // device state
-    uint64_t *d_pk = nullptr;
-    uint64_t *d_pk_tab = nullptr;      // encryption nibble table (upload_pk), or null
-    uint64_t *d_z = nullptr;           // decrypt parity table z_k = (X^k mod S)(0)
-    uint32_t z_limbs = 0;
-    uint64_t *d_s = nullptr;           // divisor scratch for hm_poly_rem_batch
-    size_t d_s_limbs = 0;
-    uint32_t *d_ws = nullptr;          // multiplier workspace
-    size_t ws_bytes = 0;
-    uint32_t *d_ws_add = nullptr;      // adder workspace (validated inputs, per-bit a_i*b_i)
-    size_t ws_add_bytes = 0;
-    uint32_t *d_mws = nullptr;         // column multiplier arena (mul_columns)
-    size_t mws_bytes = 0;
-    uint8_t *d_masks = nullptr;        // engine-drawn encryption masks (hm_encrypt_batch, masks NULL)
-    size_t masks_bytes = 0;
-    int *d_status = nullptr;
-    uint32_t cus = 256;                // compute units of the device (grid sizing)
-    hipError_t last_hip = hipSuccess;
-    // Device buffers the kernels read are never freed while the context lives: a HIP graph
-    // captured over the engine's launches holds their raw pointers.  A buffer that has to be
-    // replaced (grown, or keyed by a new key) is retired instead -- zeroed first when it holds
-    // secret-derived data -- and `generation` advances, so a graph wrapper can refuse to replay
-    // across the change (hm_ctx_generation).  hm_ctx_trim / hm_ctx_destroy free retired buffers.
-    struct Retired {
-        void *p;
-        size_t bytes;
-    };
-    std::vector<Retired> retired;
-    uint64_t generation = 0;
-};
-
 namespace {
-
-struct DeviceGuard {
-    int prev = 0;
-    explicit DeviceGuard(int dev) {
-        (void)hipGetDevice(&prev);
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        if (cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
-inline uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
-inline uint32_t words_of_bound(int64_t b) { return b < 0 ? 0u : (uint32_t)(b / 32 + 1); }
 
 uint64_t splitmix64(uint64_t &s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -132,29 +65,6 @@ void wipe(void *p, size_t n) {
     for (size_t i = 0; i < n; ++i) q[i] = 0;
 }
 
-void retire(hm_ctx *c, void *p, size_t bytes, bool secret) {
-    if (!p) return;
-    if (secret) (void)hipMemset(p, 0, bytes); // SecretKey's Drop zeroizes (context.rs:197-206)
-    c->retired.push_back({p, bytes});
-    ++c->generation;
-}
-
-// Grow-only device buffer (see hm_ctx::retired).  Allocation is synchronous, outside any
-// capture: callers size buffers on a warm-up call before a graph is captured.
-template <class T>
-hipError_t grow(hm_ctx *c, T *&p, size_t &have, size_t need, bool secret = false) {
-    if (need <= have && p) return hipSuccess;
-    hipError_t e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) return e;
-    retire(c, p, have, secret);
-    p = nullptr, have = 0;
-    e = hipMalloc(&p, need);
-    if (e != hipSuccess) return e;
-    have = need;
-    ++c->generation;
-    return hipSuccess;
-}
-
 // Host carry-less product for key generation only (setup path, runs once per key).
 std::vector<uint64_t> clmul_host(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b) {
     std::vector<uint64_t> r(a.size() + b.size(), 0);
@@ -174,17 +84,6 @@ std::vector<uint64_t> clmul_host(const std::vector<uint64_t> &a, const std::vect
     return r;
 }
 
-hm_status hip_fail(hm_ctx *c, hipError_t e) {
-    if (c) c->last_hip = e;
-    return HM_ERR_HIP;
-}
-
-#define HM_HIP(ctx, expr)                                                                         \
-    do {                                                                                          \
-        hipError_t _e = (expr);                                                                   \
-        if (_e != hipSuccess) return hip_fail((ctx), _e);                                         \
-    } while (0)
-
 uint16_t min_d_over_delta(hm_op op) { // src/impls/numbers.rs:27-50
     switch (op) {
     case HM_OP_AND: case HM_OP_OR: return 2;
@@ -193,22 +92,6 @@ uint16_t min_d_over_delta(hm_op op) { // src/impls/numbers.rs:27-50
     case HM_OP_MUL: case HM_OP_MUL_SIGNED: return 64;
     }
     return 0xFFFF;
-}
-
-bool fill_bounds(Bounds &dst, const hm_batch *b) {
-    if (!b || !b->bound || b->nbits == 0 || b->nbits > HM_MAX_BITS) return false;
-    std::memset(&dst, 0, sizeof(dst));
-    for (uint32_t i = 0; i < b->nbits; ++i) dst.b[i] = b->bound[i];
-    return true;
-}
-
-BatchArg batch_arg(const hm_batch *b) {
-    BatchArg a;
-    a.limbs = b->limbs;
-    a.degree = b->degree;
-    a.stride = hm_batch_stride(b->nbits, b->bound);
-    a.dstride = b->nbits;
-    return a;
 }
 
 // the bound of an output must cover the computed bound, bit by bit
@@ -311,14 +194,6 @@ hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n) {
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 
-hm_status check_batch(const hm_batch *b, bool need_limbs = true) {
-    if (!b || !b->bound || b->nbits == 0 || b->nbits > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
-    if (b->n && need_limbs && (!b->limbs || !b->degree)) return HM_ERR_INVALID_ARGUMENT;
-    for (uint32_t i = 0; i < b->nbits; ++i)
-        if (b->bound[i] > (1u << 30)) return HM_ERR_UNSUPPORTED;
-    return HM_OK;
-}
-
 } // namespace
 
 // =============================================================================================
@@ -387,7 +262,8 @@ void hm_ctx_destroy(hm_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     drop_secret(c);
     if (c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
-    for (void *p : {(void *)c->d_pk, (void *)c->d_pk_tab, (void *)c->d_s, (void *)c->d_ws,
+    mul_plans_release(c);
+    for (void *p : {(void *)c->d_pk, (void *)c->d_pk_tab, (void *)c->d_s,
                     (void *)c->d_ws_add, (void *)c->d_status, (void *)c->d_nonce,
                     (void *)c->d_masks, (void *)c->d_mws})
         if (p) (void)hipFree(p);
@@ -570,68 +446,14 @@ hm_status hm_add_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, ui
 
 } // extern "C"
 
-namespace {
-// Symbolic run of the carry-save multiplier over degree bounds (-1 = known null).  Also reports
-// the workspace geometry the kernel needs.
-struct MulPlan {
-    std::vector<int64_t> res;
-    uint32_t kmax = 0;
-    uint32_t slot[2] = {0, 0};
-    uint32_t tmp = 0;
-    bool ok = true;
-};
-inline int64_t bmul(int64_t x, int64_t y) { return (x < 0 || y < 0) ? -1 : x + y; }
-inline int64_t bxor(int64_t x, int64_t y) { return std::max(x, y); }
-
-MulPlan plan_mul(uint32_t L, const uint32_t *a, const uint32_t *b, int is_signed) {
-    MulPlan P;
-    P.res.assign(L, -1);
-    std::vector<int64_t> prev, cur;
-    const int64_t lim = (int64_t)1 << 30;
-    for (uint32_t i = 0; i < L; ++i) {
-        cur.clear();
-        int64_t r = -1;
-        const bool push = i + 1 < L;
-        uint32_t slot = 0;
-        for (uint32_t j = 0; j <= i; ++j) {
-            int64_t pp = (int64_t)a[j] + b[i - j];
-            P.tmp = std::max<uint32_t>(P.tmp, 2 * cap_of(a[j]) + 2 * cap_of(b[i - j]) + 2);
-            if (is_signed) {
-                int fl = (j == 0 && i - j == L - 1) + (j == L - 1 && i - j == 0);
-                if (fl & 1) pp = std::max<int64_t>(pp, 0);
-            }
-            if (push) {
-                cur.push_back(bmul(pp, r));
-                slot = std::max(slot, words_of_bound(pp) + words_of_bound(r));
-            }
-            r = bxor(r, pp);
-            if (r > lim) P.ok = false;
-        }
-        for (int64_t c : prev) {
-            if (push) {
-                cur.push_back(bmul(r, c));
-                slot = std::max(slot, words_of_bound(r) + words_of_bound(c));
-            }
-            r = bxor(r, c);
-            if (r > lim) P.ok = false;
-        }
-        P.res[i] = r;
-        P.kmax = std::max<uint32_t>(P.kmax, (uint32_t)cur.size());
-        P.slot[i & 1] = std::max(P.slot[i & 1], slot + 2);
-        prev.swap(cur);
-    }
-    return P;
-}
-} // namespace
-
 extern "C" {
 
 hm_status hm_mul_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, int is_signed,
                             uint32_t *out) {
     if (!a || !b || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
-    MulPlan P = plan_mul(L, a, b, is_signed);
-    if (!P.ok) return HM_ERR_UNSUPPORTED;
-    for (uint32_t i = 0; i < L; ++i) out[i] = (uint32_t)std::max<int64_t>(P.res[i], 0);
+    std::vector<int64_t> res;
+    if (!mul_result_bounds(L, L, a, b, is_signed != 0, res)) return HM_ERR_UNSUPPORTED;
+    for (uint32_t i = 0; i < L; ++i) out[i] = (uint32_t)std::max<int64_t>(res[i], 0);
     return HM_OK;
 }
 
@@ -805,47 +627,6 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 
-// The carry-save multiplier over the low L bits of a and b (L <= their nbits; the limbs are read
-// in place through the batches' own strides).  out has L bits.
-static hm_status mul_impl(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t L,
-                          int is_signed, hm_batch *out) {
-    MulPlan P = plan_mul(L, a->bound, b->bound, is_signed);
-    if (!P.ok) return HM_ERR_UNSUPPORTED;
-    for (uint32_t i = 0; i < L; ++i)
-        if (out->bound[i] < (uint32_t)std::max<int64_t>(P.res[i], 0)) return HM_ERR_INVALID_ARGUMENT;
-    if (a->n == 0) return HM_OK;
-    MulArgs M{};
-    uint64_t o = 0;
-    M.oIn = 0;
-    uint64_t wa = 2 * hm_batch_stride(L, a->bound), wb = 2 * hm_batch_stride(L, b->bound);
-    // (only the low L bits are staged: their limbs are the first hm_batch_stride(L) of a value)
-    M.in_words_a = (uint32_t)wa;
-    o = wa + wb;
-    for (uint32_t i = 0; i < L; ++i) {
-        M.oRes[i] = (uint32_t)o;
-        o += words_of_bound(P.res[i]) + 2;
-    }
-    M.oTmp = (uint32_t)o, o += P.tmp;
-    M.car_slot[0] = P.slot[0], M.car_slot[1] = P.slot[1];
-    M.oCar[0] = (uint32_t)o, o += (uint64_t)P.kmax * P.slot[0];
-    M.oCar[1] = (uint32_t)o, o += (uint64_t)P.kmax * P.slot[1];
-    o = (o + 63) & ~(uint64_t)63;
-    if (o >= (1ull << 32)) return HM_ERR_UNSUPPORTED;
-    M.ws_stride = o;
-    M.kmax = P.kmax;
-    M.lds_ints = 2 * L + 2 * P.kmax + 2;
-    const size_t bytes = (size_t)o * 4 * a->n;
-    DeviceGuard g(c->device);
-    HM_HIP(c, grow(c, c->d_ws, c->ws_bytes, bytes));
-    M.ws = c->d_ws;
-    M.a = batch_arg(a), M.b = batch_arg(b), M.out = batch_arg(out);
-    M.n = a->n, M.nbits = L, M.is_signed = is_signed;
-    M.status = c->d_status;
-    fill_bounds(M.ab, a), fill_bounds(M.bb, b), fill_bounds(M.ob, out);
-    const uint32_t wpb = 4;
-    return launch_mul(M, wpb, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
-
 hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,
                        hm_batch *out) {
     if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
@@ -855,7 +636,7 @@ hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_s
         if (hm_status st = check_batch(x); st) return st;
     if (a->nbits != b->nbits || a->nbits != out->nbits || a->n != b->n || a->n != out->n)
         return HM_ERR_INVALID_ARGUMENT;
-    return mul_impl(c, a, b, a->nbits, is_signed, out);
+    return mul_columns(c, a, b, a->nbits, is_signed != 0, out);
 }
 
 hm_status hm_mul_low_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t k,
@@ -867,7 +648,7 @@ hm_status hm_mul_low_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint
     if (a->nbits != b->nbits || k == 0 || k > a->nbits || out->nbits != k || a->n != b->n ||
         a->n != out->n)
         return HM_ERR_INVALID_ARGUMENT;
-    return mul_impl(c, a, b, k, 0, out);
+    return mul_columns(c, a, b, k, false, out);
 }
 
 hm_status hm_gate_batch(hm_ctx *c, hm_op gate, const hm_batch *a, const hm_batch *b,

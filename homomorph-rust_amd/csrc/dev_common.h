@@ -1,0 +1,213 @@
+// dev_common.h — device helpers shared by the gfx950 kernel translation units (kernels.hip,
+// mul_engine.hip): status flags, wave-scope fences, ciphertext-bit load/store with validation, and
+// per-lane carry-less products of "holey" operands.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "gf2_wave.h"
+
+namespace hm {
+
+__device__ __forceinline__ void flag(int *status, int code) {
+    if (status) atomicCAS(status, 0, code);
+}
+
+// wsync: order this wave's LDS writes before its later LDS reads by other lanes.  A wave's LDS
+// instructions execute in order, so only the compiler must be kept from reordering (wavefront
+// scope emits no wait).  gsync: the same for GLOBAL memory, where a lane's load must not overtake
+// another lane's earlier store: workgroup scope drains vmcnt/lgkmcnt.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void gsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
+
+// Load one ciphertext bit (u64 limbs, exact degree `deg`) into 32-bit words at dst.
+// The degree word is validated against the limbs (top bit set, nothing above it).
+// Returns the word count (0 for the null polynomial).
+__device__ inline int load_bit(const uint64_t *__restrict__ src, uint32_t deg, uint32_t bound,
+                        uint32_t *__restrict__ dst, int *status) {
+    const int lane = lane_id();
+    if (deg > bound) {
+        if (lane == 0) flag(status, HM_ERR_BAD_INPUT);
+        return 0;
+    }
+    const int nl = (int)(deg / 64) + 1;
+    const int cap = (int)(bound / 64) + 1;
+    const uint32_t tb = deg % 64;
+    bool bad = false;
+    for (int g = lane; g < cap; g += kWave) {
+        uint64_t v = src[g];
+        if (g >= nl) { // limbs above the degree must be zero (layout invariant)
+            bad |= v != 0;
+            continue;
+        }
+        if (g == nl - 1) {
+            const uint64_t keep = (~0ull) >> (63 - tb);
+            bad |= (v & ~keep) != 0;
+            v &= keep;
+            if (deg > 0 && !((v >> tb) & 1ull)) bad = true;
+        }
+        dst[2 * g] = (uint32_t)v;
+        dst[2 * g + 1] = (uint32_t)(v >> 32);
+    }
+    if (__any(bad) && lane == 0) flag(status, HM_ERR_BAD_INPUT);
+    if (deg == 0) {
+        const uint32_t w0 = rfl((uint32_t)src[0]);
+        if (!(w0 & 1u)) return 0;
+    }
+    return (int)(deg / 32) + 1;
+}
+
+// dst (cap limbs) = X ^ C; writes the exact degree; returns it (-1 = null).
+__device__ inline int store_xor_bit(const uint32_t *X, int nx, const uint32_t *C, int nc,
+                             uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
+                             int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int n = max(nx, nc);
+    const int total = max(cap, (n + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        uint32_t lo = (w < nx ? X[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        uint32_t hi = (w + 1 < nx ? X[w + 1] : 0u) ^ (w + 1 < nc ? C[w + 1] : 0u);
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+__device__ __forceinline__ int words_of(int deg) { return deg >= 0 ? nwords(deg) : 0; }
+
+// dst (cap limbs) = A ^ B ^ C (output bit of the adder); writes the exact degree.
+__device__ inline int store_xor3_bit(const uint32_t *Aw, int na, const uint32_t *Bw, int nb,
+                              const uint32_t *C, int nc, uint64_t *__restrict__ dst,
+                              uint32_t bound, uint32_t *deg_out, int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int n = max(max(na, nb), nc);
+    const int total = max(cap, (n + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        uint32_t lo = (w < na ? Aw[w] : 0u) ^ (w < nb ? Bw[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        uint32_t hi = (w + 1 < na ? Aw[w + 1] : 0u) ^ (w + 1 < nb ? Bw[w + 1] : 0u) ^
+                      (w + 1 < nc ? C[w + 1] : 0u);
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+// Small products (fresh operands: 9 words at d+dp = 256) use a short uniform chunk; the carry
+// product P * carry uses a chunk that covers P (25 words at d+dp = 256) in one pass.
+constexpr int kQSmall = 10;
+constexpr int kQBig = 25;
+
+// ---------------------------------------------------------------------------------------------
+// Per-lane carry-less product word by integer multiplication of "holey" operands.
+// Split u and v by bit position mod 4 (u_a = u & M_a, M_a = 0x11111111 << a).  In the integer
+// product u_a * v_b every set bit pair lands on a position == a+b (mod 4), and at most 8 pairs
+// land on any one position (8 bits per holey word), so the column counts never carry out of
+// their 4-bit field: bit p of u_a*v_b is the GF(2) coefficient sum at p.  XOR the 4 products of
+// each residue class c, keep the positions == c:  clmul(u, v) = OR_c (M_c & XOR_{a+b=c} u_a v_b).
+// v_mul_lo_u32 / v_mul_hi_u32 give the two halves of the 64-bit product at the rate of a shift
+// (measured), i.e. 16 multiplies replace 32 (funnel + bfe + bitop3) bit steps.
+// Masking commutes with XOR, so classes are accumulated over q and masked once per word.
+struct Holey {
+    uint32_t h[4];
+    __device__ __forceinline__ explicit Holey(uint32_t v) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) h[a] = v & (0x11111111u << a);
+    }
+};
+
+// z[c] ^= low halves of U (x) V1  ^  high halves of U (x) V0   (residue class c)
+__device__ __forceinline__ void holey_acc(uint32_t z[4], const Holey &U, const Holey &V1,
+                                          const Holey &V0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int b = (c - a) & 3;
+            lo ^= U.h[a] * V1.h[b];
+            hi ^= __umulhi(U.h[a], V0.h[b]);
+        }
+        z[c] ^= lo ^ hi;
+    }
+}
+
+__device__ __forceinline__ uint32_t holey_fold(const uint32_t z[4]) {
+    return (z[0] & 0x11111111u) | (z[1] & 0x22222222u) | (z[2] & 0x44444444u) |
+           (z[3] & 0x88888888u);
+}
+
+// Word m of U*V (U: nu words, V: nv words): XOR over q of low(U_q V_{m-q}) ^ high(U_q V_{m-q-1}).
+// Used where lanes work on DIFFERENT products (no uniform operand), i.e. the adder's pre-phase.
+__device__ __forceinline__ uint32_t clmul_word(const uint32_t *__restrict__ pu, int nu,
+                                               const uint32_t *__restrict__ pv, int nv, int m) {
+    uint32_t z[4] = {0u, 0u, 0u, 0u};
+    const int qlo = max(0, m - nv), qhi = min(nu - 1, m);
+    if (qlo > qhi) return 0u;
+    int k = m - qlo;
+    Holey V1(k < nv ? pv[k] : 0u);
+    for (int q = qlo; q <= qhi; ++q, --k) {
+        const Holey V0((k >= 1 && k - 1 < nv) ? pv[k - 1] : 0u);
+        holey_acc(z, Holey(pu[q]), V1, V0);
+        V1 = V0; // V_{m-q-1} is the next q's V_{m-q}
+    }
+    return holey_fold(z);
+}
+
+// One row of a product: out[k] ^= word k of u * V for k = 0..nv (out in LDS, shared by the
+// lanes that own the other rows, hence ds_xor).  Each 32x32 product is formed whole: 16
+// v_mad_u64_u32 give both halves, the low half goes to word k and the high half to word k+1.
+__device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__restrict__ pv, int nv,
+                                              uint32_t *out) {
+    const Holey U(u);
+    uint32_t hiprev = 0u;
+    for (int k = 0; k <= nv; ++k) {
+        uint32_t lo = 0u, hi = 0u;
+        if (k < nv) {
+            const Holey V(pv[k]);
+            uint64_t z[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) z[(a + b) & 3] ^= (uint64_t)U.h[a] * V.h[b];
+            uint32_t zl[4], zh[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) zl[c] = (uint32_t)z[c], zh[c] = (uint32_t)(z[c] >> 32);
+            lo = holey_fold(zl), hi = holey_fold(zh);
+        }
+        const uint32_t w = lo ^ hiprev;
+        if (w) atomicXor(&out[k], w);
+        hiprev = hi;
+    }
+}
+
+__device__ __forceinline__ int bitwords(int degp1) { return degp1 ? ((degp1 - 1) >> 5) + 1 : 0; }
+
+} // namespace hm

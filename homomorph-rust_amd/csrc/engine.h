@@ -75,7 +75,7 @@ struct DecArgs {
     uint32_t ucap;   // every bit has exactly ucap <= 8 limbs (fresh ciphertexts), else 0
 };
 
-// Gates and the carry-save multiplier keep their intermediates in a per-value global workspace.
+// Gates keep their intermediates in LDS, one wavefront per value.
 struct GateArgs {
     int op;
     BatchArg a, b, out;
@@ -86,22 +86,70 @@ struct GateArgs {
     Bounds ab, bb, ob;
 };
 
-struct MulArgs {
-    BatchArg a, b, out;
-    uint64_t n;
-    uint32_t nbits;
-    int is_signed;
-    uint32_t *ws;        // workspace, ws_stride words per value
-    uint64_t ws_stride;
-    uint32_t oIn, in_words_a;   // inputs a then b (words) at ws + oIn
-    uint32_t oRes[HM_MAX_BITS]; // word offsets of result columns
-    uint32_t oTmp;              // partial-product scratch
-    uint32_t oCar[2];           // two carry lists (column parity)
-    uint32_t car_slot[2];       // words per carry slot in each list
-    uint32_t kmax;              // max carries pushed by one column
-    uint32_t lds_ints;          // per-wave LDS ints: 2*nbits + 2*kmax + 1
+// Column-parallel carry-save multiplier (mul_engine.hip, mul_host.cpp).  Column i of
+// mul_unsigned_internal (common.rs:66-105) XORs its items x_0..x_{n-1} (the partial products
+// a_j b_{i-j}, then the previous column's carries) into result_i and pushes the carry
+// (x_0 ^ .. ^ x_{t-1}) * x_t before each XOR.  With the prefixes p_t = x_0 ^ .. ^ x_{t-1}
+// materialised (a scan), every carry of a column is an independent product p_t * x_t, so a column
+// is three launches over the whole batch: partial products, prefix scan (its last prefix is the
+// output bit), and the carry products, tiled over the chip.  Polynomials live in a per-value
+// arena of u32 words at static offsets (slots, capacity = bound/32 + 1 rounded up to 4 words,
+// always zero above the degree); deg1[slot * nv + e] = degree + 1 of value e (0 = null).
+struct MulSlot {
+    uint32_t off;   // u32-word offset in a value's arena
+    uint32_t words; // capacity (multiple of 4)
+};
+struct MulBase {
+    uint32_t *arena;
+    uint64_t astride; // arena words per value
+    uint32_t *deg1;
+    uint64_t nv;      // values in this chunk (deg1 row length)
+    const MulSlot *slots;
+    uint64_t e0;      // first value of the chunk in the caller's batches
     int *status;
-    Bounds ab, bb, ob;
+};
+struct MulStageArgs {
+    MulBase B;
+    BatchArg a, b;
+    uint32_t K;       // input bits staged: a_j -> slot j, b_j -> slot K + j
+    Bounds ab, bb;
+};
+struct MulPPTask {
+    uint32_t a, b, out, flip; // out = a * b (+1 when flip: mul_signed_internal, common.rs:123-126)
+};
+struct MulPPArgs {
+    MulBase B;
+    const MulPPTask *tasks;
+    uint32_t ntasks;
+};
+struct MulScanArgs {
+    MulBase B;
+    const uint32_t *items;  // nitems slot ids, in the reference's XOR order
+    const uint32_t *prefix; // nitems - 1 slot ids: p_1 .. p_{n-1}
+    uint32_t nitems;
+    uint32_t chunks;        // 256-word chunks per value (of the widest prefix)
+    uint32_t res;           // degree slot of the result (output bit i)
+    BatchArg out;
+    uint32_t out_off, out_cap; // output bit i: limb offset within a value, capacity in limbs
+};
+struct MulProdTask {
+    uint32_t u, v, out; // out = u * v; u is the operand with fewer words (the uniform one)
+};
+struct MulTile {
+    uint32_t task, base; // output words [base, base + 64 W) of task
+};
+struct MulProdArgs {
+    MulBase B;
+    const MulProdTask *tasks;
+    const MulTile *tiles;
+    uint32_t ntiles;
+};
+struct MulFinalArgs {
+    MulBase B;
+    const uint32_t *res; // K degree slots of the output bits
+    uint32_t K;
+    BatchArg out;
+    Bounds ob;
 };
 
 struct PolyArgs {
@@ -133,7 +181,12 @@ int launch_add(const AddArgs &a, void *stream);
 int launch_encrypt(const EncArgs &a, void *stream);
 int launch_decrypt(const DecArgs &a, void *stream);
 int launch_gate(const GateArgs &a, void *stream);
-int launch_mul(const MulArgs &a, uint32_t waves_per_block, void *stream);
+int launch_mul_stage(const MulStageArgs &a, void *stream);
+int launch_mul_pp(const MulPPArgs &a, void *stream);
+int launch_mul_scan(const MulScanArgs &a, void *stream);
+int launch_mul_prod(const MulProdArgs &a, uint32_t w, void *stream);
+int launch_mul_final(const MulFinalArgs &a, void *stream);
+constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches
 int launch_poly_add(const PolyArgs &a, void *stream);
 int launch_poly_mul(const PolyArgs &a, void *stream);
 int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);

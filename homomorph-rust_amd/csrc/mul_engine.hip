@@ -1,0 +1,243 @@
+// mul_engine.hip — gfx950 kernels of the column-parallel carry-save multiplier
+// (mul_unsigned_internal / mul_signed_internal, src/impls/numbers/common.rs:66-155).
+//
+// The reference walks column i's items x_0..x_{n-1} (partial products a_j b_{i-j}, then the
+// previous column's carries) sequentially:  carries.push(result * x_t); result ^= x_t.  The
+// carry pushed before item t is p_t * x_t with p_t = x_0 ^ .. ^ x_{t-1} (the running result), so
+// once the prefixes are materialised every carry of a column is an independent product and the
+// whole batch's column runs as three wide launches:
+//   mul_pp_kernel     partial products a_j * b_{i-j} (fresh x fresh, per-lane holey multiplies)
+//   mul_scan_kernel   prefixes p_1..p_{n-1} and the output bit p_n (XOR streams over 256-word
+//                     chunks, lanes over words, one uint4 per lane)
+//   mul_prod_kernel   carries p_t * x_t, one wavefront per (value, 64*W-word output tile):
+//                     Horner over the uniform operand's bits with scalar decisions (gf2_wave.h)
+// The products are exact (GF(2)[X] has no zero divisors: deg = deg u + deg v), the prefixes'
+// degrees come from the words, so every polynomial is bit-identical to the reference's.
+#include "dev_common.h"
+
+namespace hm {
+
+__device__ __forceinline__ uint32_t *slot_ptr(const MulBase &B, uint32_t s, uint64_t e) {
+    return B.arena + e * B.astride + B.slots[s].off;
+}
+
+// one ciphertext bit (u64 limbs + exact degree) -> arena slot (u32 words, zero-filled to the
+// slot's capacity), validated as load_bit does; writes deg1.
+__device__ void stage_one(const MulBase &B, const uint64_t *src, uint32_t deg, uint32_t bound,
+                          uint32_t slot, uint64_t e) {
+    const int lane = lane_id();
+    uint32_t *dst = slot_ptr(B, slot, e);
+    const uint32_t words = B.slots[slot].words;
+    const uint32_t cap = bound / 64 + 1;
+    bool bad = deg > bound;
+    const uint32_t nl = bad ? 0u : deg / 64 + 1, tb = deg % 64;
+    uint32_t w0 = 0u;
+    for (uint32_t g = lane; 2 * g < words; g += kWave) {
+        uint64_t v = (g < cap) ? src[g] : 0ull;
+        if (g >= nl) {
+            bad |= v != 0;
+            v = 0;
+        } else if (g == nl - 1) {
+            const uint64_t keep = (~0ull) >> (63 - tb);
+            bad |= (v & ~keep) != 0;
+            v &= keep;
+            if (deg > 0 && !((v >> tb) & 1ull)) bad = true;
+        }
+        if (g == 0) w0 = (uint32_t)v;
+        dst[2 * g] = (uint32_t)v;
+        if (2 * g + 1 < words) dst[2 * g + 1] = (uint32_t)(v >> 32);
+    }
+    for (uint32_t g = (words + 1) / 2 + lane; g < cap; g += kWave) bad |= src[g] != 0;
+    if (__any(bad) && lane == 0) flag(B.status, HM_ERR_BAD_INPUT);
+    w0 = (uint32_t)__shfl((int)w0, 0, 64);
+    if (lane == 0) {
+        const bool null = deg == 0 && !(w0 & 1u);
+        B.deg1[(uint64_t)slot * B.nv + e] = (bad || null) ? 0u : deg + 1;
+    }
+}
+
+// one wave per (value, input bit): a_j -> slot j, b_j -> slot K + j
+__global__ void __launch_bounds__(256) mul_stage_kernel(MulStageArgs S) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint64_t e = g / (2 * S.K);
+    const uint32_t t = (uint32_t)(g % (2 * S.K));
+    if (e >= S.B.nv) return;
+    const bool isb = t >= S.K;
+    const uint32_t j = isb ? t - S.K : t;
+    const BatchArg &A = isb ? S.b : S.a;
+    const Bounds &bd = isb ? S.bb : S.ab;
+    uint32_t off = 0;
+    for (uint32_t q = 0; q < j; ++q) off += cap_of(bd.b[q]);
+    const uint64_t ge = S.B.e0 + e;
+    stage_one(S.B, A.limbs + ge * A.stride + off, rfl(A.degree[ge * A.dstride + j]), bd.b[j], t, e);
+}
+
+int launch_mul_stage(const MulStageArgs &S, void *stream) {
+    const uint64_t waves = S.B.nv * 2 * S.K;
+    if (!waves) return 0;
+    hipLaunchKernelGGL(mul_stage_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, S);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// exact top bit of a word range spread over the wave (lane-local top word index `tw`, -1 = none)
+__device__ __forceinline__ int wave_topbit(int tw, uint32_t v) {
+    const int lb = tw >= 0 ? tw * 32 + 31 - __builtin_clz(v) : -1;
+    return wave_max_i32(lb);
+}
+
+// one wave per (value, partial product): out = a * b (+1), lanes over output words
+__global__ void __launch_bounds__(256) mul_pp_kernel(MulPPArgs P) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint64_t e = g / P.ntasks;
+    const uint32_t k = (uint32_t)(g % P.ntasks);
+    if (e >= P.B.nv) return;
+    const MulPPTask T = P.tasks[k];
+    const uint32_t da = P.B.deg1[(uint64_t)T.a * P.B.nv + e], db = P.B.deg1[(uint64_t)T.b * P.B.nv + e];
+    const int na = bitwords((int)rfl(da)), nb = bitwords((int)rfl(db));
+    const uint32_t *A = slot_ptr(P.B, T.a, e), *Bp = slot_ptr(P.B, T.b, e);
+    uint32_t *O = slot_ptr(P.B, T.out, e);
+    const uint32_t words = P.B.slots[T.out].words;
+    int tw = -1;
+    uint32_t tv = 0;
+    for (uint32_t m = lane_id(); m < words; m += kWave) {
+        uint32_t w = (na && nb) ? clmul_word(A, na, Bp, nb, (int)m) : 0u;
+        if (m == 0 && T.flip) w ^= 1u;
+        O[m] = w;
+        if (w) tw = (int)m, tv = w;
+    }
+    const int top = wave_topbit(tw, tv);
+    if (lane_id() == 0) P.B.deg1[(uint64_t)T.out * P.B.nv + e] = (uint32_t)(top + 1);
+}
+
+int launch_mul_pp(const MulPPArgs &P, void *stream) {
+    const uint64_t waves = P.B.nv * P.ntasks;
+    if (!waves) return 0;
+    hipLaunchKernelGGL(mul_pp_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// one wave per (value, 256-word chunk): acc ^= x_t chunk, store p_{t+1} chunk, track degrees.
+// Slots are zero above their degree and capacities are multiples of 4 words, so every item and
+// prefix is read / written as whole uint4s up to its capacity.
+__global__ void __launch_bounds__(256) mul_scan_kernel(MulScanArgs S) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint64_t e = g / S.chunks;
+    const uint32_t c0 = (uint32_t)(g % S.chunks) * 256u;
+    if (e >= S.B.nv) return;
+    const int lane = lane_id();
+    const uint32_t w = c0 + 4u * (uint32_t)lane;
+    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t t = 0; t < S.nitems; ++t) {
+        const uint32_t it = S.items[t];
+        const MulSlot si = S.B.slots[it];
+        if (w < si.words) {
+            const uint4 v = *(const uint4 *)(S.B.arena + e * S.B.astride + si.off + w);
+            acc.x ^= v.x, acc.y ^= v.y, acc.z ^= v.z, acc.w ^= v.w;
+        }
+        int tw = -1;
+        uint32_t tv = 0;
+        if (acc.x) tw = (int)w, tv = acc.x;
+        if (acc.y) tw = (int)w + 1, tv = acc.y;
+        if (acc.z) tw = (int)w + 2, tv = acc.z;
+        if (acc.w) tw = (int)w + 3, tv = acc.w;
+        const uint32_t dslot = t + 1 < S.nitems ? S.prefix[t] : S.res;
+        if (t + 1 < S.nitems) {
+            const MulSlot sp = S.B.slots[dslot];
+            if (w < sp.words) *(uint4 *)(S.B.arena + e * S.B.astride + sp.off + w) = acc;
+        } else {
+            // the output bit: u32 words into the u64 limbs (little-endian), zeros up to capacity
+            uint32_t *o = (uint32_t *)(S.out.limbs + (S.B.e0 + e) * S.out.stride + S.out_off);
+            const uint32_t ow = 2 * S.out_cap;
+            if (w < ow) *(uint2 *)(o + w) = make_uint2(acc.x, acc.y);
+            if (w + 2 < ow) *(uint2 *)(o + w + 2) = make_uint2(acc.z, acc.w);
+        }
+        // degree + 1 of this prefix: the chunk's top bit, max over chunks
+        const uint64_t m = __ballot(tw >= 0);
+        if (m) {
+            const int hl = 63 - __builtin_clzll(m);
+            if (lane == hl) atomicMax(&S.B.deg1[(uint64_t)dslot * S.B.nv + e],
+                                      (uint32_t)(tw * 32 + 32 - __builtin_clz(tv)));
+        }
+    }
+}
+
+int launch_mul_scan(const MulScanArgs &S, void *stream) {
+    const uint64_t waves = S.B.nv * S.chunks;
+    if (!waves || !S.nitems) return 0;
+    hipLaunchKernelGGL(mul_scan_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, S);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// One wave per (value, tile): output words [base, base + 64 W) of u * v.  The operand with fewer
+// words is the uniform one (its bits become scalar decisions); QC words of it per Horner pass.
+constexpr int kMulQC = 10;
+
+template <int W>
+__global__ void __launch_bounds__(256) mul_prod_kernel(MulProdArgs P) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint64_t e = g / P.ntiles;
+    const uint32_t k = (uint32_t)(g % P.ntiles);
+    if (e >= P.B.nv) return;
+    const MulTile tl = P.tiles[k];
+    const MulProdTask T = P.tasks[tl.task];
+    const uint32_t du = rfl(P.B.deg1[(uint64_t)T.u * P.B.nv + e]);
+    const uint32_t dv = rfl(P.B.deg1[(uint64_t)T.v * P.B.nv + e]);
+    uint32_t *O = slot_ptr(P.B, T.out, e);
+    const int nout = (int)P.B.slots[T.out].words;
+    const int base = (int)rfl(tl.base);
+    if (du == 0 || dv == 0) { // a null operand: the carry is null (zero-filled slot)
+        for (int j = 0; j < W; ++j) {
+            const int w = base + lane_id() * W + j;
+            if (w < nout) O[w] = 0u;
+        }
+    } else {
+        const uint32_t *U = slot_ptr(P.B, T.u, e), *V = slot_ptr(P.B, T.v, e);
+        const int nu = bitwords((int)du), nv = bitwords((int)dv);
+        if (base == 0)
+            mul_tile<W, kMulQC, false, pair_mode<W>(), false>(U, nu, V, nv, nullptr, 0, O, nout, 0);
+        else
+            mul_tile<W, kMulQC, true, pair_mode<W>(), false>(U, nu, V, nv, nullptr, 0, O, nout, base);
+    }
+    if (base == 0 && lane_id() == 0)
+        P.B.deg1[(uint64_t)T.out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+}
+
+int launch_mul_prod(const MulProdArgs &P, uint32_t w, void *stream) {
+    const uint64_t waves = P.B.nv * P.ntiles;
+    if (!waves) return 0;
+    const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+    switch (w) {
+    case 1: hipLaunchKernelGGL(mul_prod_kernel<1>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 2: hipLaunchKernelGGL(mul_prod_kernel<2>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 4: hipLaunchKernelGGL(mul_prod_kernel<4>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 8: hipLaunchKernelGGL(mul_prod_kernel<8>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 12: hipLaunchKernelGGL(mul_prod_kernel<12>, grid, block, 0, (hipStream_t)stream, P); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// output degree words (exact; null -> 0) and the capacity check
+__global__ void __launch_bounds__(256) mul_final_kernel(MulFinalArgs F) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t e = t / F.K;
+    const uint32_t i = (uint32_t)(t % F.K);
+    if (e >= F.B.nv) return;
+    const uint32_t d1 = F.B.deg1[(uint64_t)F.res[i] * F.B.nv + e];
+    const uint32_t d = d1 ? d1 - 1 : 0u;
+    if (d > F.ob.b[i]) flag(F.B.status, HM_ERR_CAPACITY);
+    F.out.degree[(F.B.e0 + e) * F.out.dstride + i] = d;
+}
+
+int launch_mul_final(const MulFinalArgs &F, void *stream) {
+    const uint64_t threads = F.B.nv * F.K;
+    if (!threads) return 0;
+    hipLaunchKernelGGL(mul_final_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, F);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace hm

@@ -1,0 +1,334 @@
+// mul_host.cpp — host side of the column-parallel carry-save multiplier (mul_engine.hip).
+//
+// A plan is the symbolic run of mul_unsigned_internal / mul_signed_internal
+// (src/impls/numbers/common.rs:66-155) over static degree bounds: every polynomial the reference
+// builds gets a slot (a static offset in a per-value arena of u32 words, capacity from its bound)
+// and a degree slot, and every column becomes three launches over the whole batch:
+//   partial products  pp_j = a_j * b_{i-j}              (j = 0..i; +1 at the signed corners)
+//   prefix scan       p_t = x_0 ^ .. ^ x_{t-1}, result_i = p_n (written to the output bit)
+//   carry products    c_t = p_t * x_t                    (t >= 1; column i < K-1 only)
+// Items are the column's partial products, then the previous column's carries, in the
+// reference's order.  Polynomials that are null by construction (the carry pushed before a
+// column's first item: result_i is still zero) are not materialised: XOR with null is the
+// identity and a product with null is null, so dropping them changes no output bit.
+// Plans (with their device task tables) are cached per context, keyed by the operand bounds.
+#include <algorithm>
+#include <cstring>
+#include <memory>
+
+#include "ctx.h"
+
+namespace hm {
+
+namespace {
+
+constexpr int64_t kBoundLimit = (int64_t)1 << 30;
+constexpr uint32_t kNW = sizeof(kMulTileW) / sizeof(kMulTileW[0]);
+
+inline uint32_t slot_words(int64_t bound) { return ((uint32_t)(bound / 32) + 1 + 3) & ~3u; }
+
+// signed circuit: pp[0][L-1] and pp[L-1][0] get ^1 (common.rs:123-126); at L = 1 both are pp[0][0]
+inline bool pp_flip(bool is_signed, uint32_t L, uint32_t i, uint32_t j) {
+    if (!is_signed || i != L - 1) return false;
+    const int f = (j == 0) + (j == L - 1);
+    return f & 1;
+}
+
+} // namespace
+
+struct MulPlan {
+    // key
+    uint32_t L = 0, K = 0;
+    bool is_signed = false;
+    std::vector<uint32_t> ab, bb;
+    // geometry
+    std::vector<MulSlot> slots;
+    uint64_t astride = 0; // arena words per value
+    std::vector<int64_t> res_bound;
+    struct Col {
+        uint32_t pp, npp;          // MulPPTask offset / count (in tasks)
+        uint32_t items, nitems;    // u32 offset of the item slot ids
+        uint32_t prefix;           // u32 offset of the prefix slot ids (nitems - 1)
+        uint32_t res;              // result degree slot
+        uint32_t maxwords;         // widest prefix / result
+        uint32_t prod;             // MulProdTask offset (in tasks)
+        uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
+    };
+    std::vector<Col> cols;
+    std::vector<uint32_t> res_slots;
+    // host tables, then one device copy
+    std::vector<MulPPTask> pp;
+    std::vector<uint32_t> lists;
+    std::vector<MulProdTask> prod;
+    std::vector<MulTile> tiles;
+    uint8_t *d_tab = nullptr;
+    size_t tab_bytes = 0;
+    size_t off_slots = 0, off_pp = 0, off_lists = 0, off_prod = 0, off_tiles = 0, off_res = 0;
+    uint64_t work = 0; // word-pair products (statistics)
+};
+
+namespace {
+
+struct Region {
+    uint64_t used = 0, max = 0;
+    uint64_t base = 0;
+};
+
+// Symbolic run.  Slot offsets are first relative to their region (in / pp / prefix / carries of
+// even columns / carries of odd columns); regions are placed once their maxima are known.
+bool build_plan(MulPlan &P) {
+    const uint32_t K = P.K;
+    enum { IN, PP, PRE, CA, CB, NREG };
+    Region reg[NREG];
+    std::vector<uint8_t> slot_reg;
+    auto new_slot = [&](int r, int64_t bound) -> uint32_t {
+        const uint32_t w = bound < 0 ? 0u : slot_words(bound);
+        P.slots.push_back({(uint32_t)reg[r].used, w});
+        slot_reg.push_back((uint8_t)r);
+        reg[r].used += w;
+        reg[r].max = std::max(reg[r].max, reg[r].used);
+        return (uint32_t)P.slots.size() - 1;
+    };
+    for (uint32_t j = 0; j < K; ++j) new_slot(IN, P.ab[j]);
+    for (uint32_t j = 0; j < K; ++j) new_slot(IN, P.bb[j]);
+    struct Item {
+        uint32_t slot;
+        int64_t bound;
+    };
+    std::vector<Item> prev;
+    P.res_bound.assign(K, -1);
+    for (uint32_t i = 0; i < K; ++i) {
+        MulPlan::Col col{};
+        reg[PP].used = 0;
+        reg[PRE].used = 0;
+        const int creg = (i & 1) ? CB : CA;
+        reg[creg].used = 0;
+        std::vector<Item> items;
+        col.pp = (uint32_t)P.pp.size();
+        for (uint32_t j = 0; j <= i; ++j) {
+            const int64_t bnd = (int64_t)P.ab[j] + P.bb[i - j];
+            if (bnd > kBoundLimit) return false;
+            const uint32_t s = new_slot(PP, bnd);
+            P.pp.push_back({j, K + (i - j), s, pp_flip(P.is_signed, P.L, i, j) ? 1u : 0u});
+            items.push_back({s, bnd});
+        }
+        col.npp = (uint32_t)P.pp.size() - col.pp;
+        items.insert(items.end(), prev.begin(), prev.end());
+        const bool push = i + 1 < K;
+        std::vector<Item> cur;
+        col.items = (uint32_t)P.lists.size();
+        col.nitems = (uint32_t)items.size();
+        for (auto &x : items) P.lists.push_back(x.slot);
+        col.prefix = (uint32_t)P.lists.size();
+        col.prod = (uint32_t)P.prod.size();
+        int64_t pb = -1;          // bound of p_t (the running result before item t)
+        uint32_t pslot = 0;       // slot of p_t (t >= 1)
+        uint32_t maxw = 0;
+        for (size_t t = 0; t < items.size(); ++t) {
+            const Item &x = items[t];
+            if (push && pb >= 0) { // carries.push(result & x_t) (common.rs:83-87, :93-96)
+                const int64_t cbnd = pb + x.bound;
+                if (cbnd > kBoundLimit) return false;
+                const uint32_t cs = new_slot(creg, cbnd);
+                const uint32_t wp = P.slots[pslot].words, wx = P.slots[x.slot].words;
+                // the operand with fewer words is the uniform one (its bits are the decisions)
+                if (wp <= wx) P.prod.push_back({pslot, x.slot, cs});
+                else P.prod.push_back({x.slot, pslot, cs});
+                P.work += (uint64_t)(pb / 32 + 1) * (uint64_t)(x.bound / 32 + 1);
+                cur.push_back({cs, cbnd});
+            }
+            pb = std::max(pb, x.bound); // result ^= x_t
+            maxw = std::max(maxw, slot_words(pb));
+            if (t + 1 < items.size()) {
+                pslot = new_slot(PRE, pb);
+                P.lists.push_back(pslot);
+            }
+        }
+        col.maxwords = maxw;
+        col.res = new_slot(PRE, -1); // degree-only slot (the output bit)
+        P.res_slots.push_back(col.res);
+        P.res_bound[i] = pb;
+        // tiles of this column's products, grouped by per-lane width
+        std::vector<MulTile> byw[kNW];
+        for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
+            const uint32_t nout = P.slots[P.prod[k].out].words;
+            const uint32_t need = (nout + 63) / 64;
+            uint32_t wc = kNW - 1;
+            for (uint32_t q = 0; q < kNW; ++q)
+                if (kMulTileW[q] >= need) {
+                    wc = q;
+                    break;
+                }
+            const uint32_t span = 64 * kMulTileW[wc];
+            for (uint32_t base = 0; base < nout; base += span) byw[wc].push_back({k - col.prod, base});
+        }
+        for (uint32_t q = 0; q < kNW; ++q) {
+            col.tiles[q] = (uint32_t)P.tiles.size();
+            col.ntiles[q] = (uint32_t)byw[q].size();
+            P.tiles.insert(P.tiles.end(), byw[q].begin(), byw[q].end());
+        }
+        P.cols.push_back(col);
+        prev.swap(cur);
+    }
+    // place the regions and make the offsets absolute
+    uint64_t base = 0;
+    for (int r = 0; r < NREG; ++r) {
+        reg[r].base = base;
+        base += (reg[r].max + 3) & ~(uint64_t)3;
+    }
+    if (base >= (1ull << 32)) return false;
+    for (size_t s = 0; s < P.slots.size(); ++s) P.slots[s].off += (uint32_t)reg[slot_reg[s]].base;
+    P.astride = std::max<uint64_t>(base, 4);
+    return true;
+}
+
+hm_status upload_plan(hm_ctx *c, MulPlan &P) {
+    auto align = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    size_t o = 0;
+    P.off_slots = o, o = align(o + P.slots.size() * sizeof(MulSlot));
+    P.off_pp = o, o = align(o + P.pp.size() * sizeof(MulPPTask));
+    P.off_lists = o, o = align(o + P.lists.size() * 4);
+    P.off_prod = o, o = align(o + P.prod.size() * sizeof(MulProdTask));
+    P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
+    P.off_res = o, o = align(o + P.res_slots.size() * 4);
+    std::vector<uint8_t> h(std::max<size_t>(o, 16), 0);
+    auto put = [&](size_t off, const void *src, size_t n) {
+        if (n) std::memcpy(h.data() + off, src, n);
+    };
+    put(P.off_slots, P.slots.data(), P.slots.size() * sizeof(MulSlot));
+    put(P.off_pp, P.pp.data(), P.pp.size() * sizeof(MulPPTask));
+    put(P.off_lists, P.lists.data(), P.lists.size() * 4);
+    put(P.off_prod, P.prod.data(), P.prod.size() * sizeof(MulProdTask));
+    put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
+    put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
+    DeviceGuard g(c->device);
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    HM_HIP(c, hipMalloc(&P.d_tab, h.size()));
+    P.tab_bytes = h.size();
+    HM_HIP(c, hipMemcpy(P.d_tab, h.data(), h.size(), hipMemcpyHostToDevice));
+    return HM_OK;
+}
+
+constexpr size_t kMaxPlans = 8;
+
+hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const uint32_t *bb,
+                   bool is_signed, MulPlan *&out) {
+    for (MulPlan *p : c->mul_plans)
+        if (p->L == L && p->K == K && p->is_signed == is_signed &&
+            std::equal(p->ab.begin(), p->ab.end(), ab) && std::equal(p->bb.begin(), p->bb.end(), bb)) {
+            out = p;
+            return HM_OK;
+        }
+    auto P = std::make_unique<MulPlan>();
+    P->L = L, P->K = K, P->is_signed = is_signed;
+    P->ab.assign(ab, ab + K), P->bb.assign(bb, bb + K);
+    if (!build_plan(*P)) return HM_ERR_UNSUPPORTED;
+    if (hm_status st = upload_plan(c, *P); st) {
+        if (P->d_tab) (void)hipFree(P->d_tab);
+        return st;
+    }
+    if (c->mul_plans.size() >= kMaxPlans) { // a captured graph may still hold the table: retire it
+        MulPlan *old = c->mul_plans.front();
+        retire(c, old->d_tab, old->tab_bytes, false);
+        delete old;
+        c->mul_plans.erase(c->mul_plans.begin());
+    }
+    out = P.release();
+    c->mul_plans.push_back(out);
+    return HM_OK;
+}
+
+} // namespace
+
+bool mul_result_bounds(uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,
+                       bool is_signed, std::vector<int64_t> &res) {
+    MulPlan P;
+    P.L = nbits, P.K = K, P.is_signed = is_signed;
+    P.ab.assign(a, a + K), P.bb.assign(b, b + K);
+    if (!build_plan(P)) return false;
+    res = P.res_bound;
+    return true;
+}
+
+void mul_plans_release(hm_ctx *c) {
+    for (MulPlan *p : c->mul_plans) {
+        if (p->d_tab) (void)hipFree(p->d_tab);
+        delete p;
+    }
+    c->mul_plans.clear();
+}
+
+hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t K, bool is_signed,
+                      hm_batch *out) {
+    const uint32_t L = a->nbits;
+    if (b->nbits != L || K == 0 || K > L || out->nbits != K) return HM_ERR_INVALID_ARGUMENT;
+    const bool flip = is_signed && K == L; // the signed corners are in column L-1 only
+    MulPlan *P = nullptr;
+    if (hm_status st = get_plan(c, L, K, a->bound, b->bound, flip, P); st) return st;
+    for (uint32_t i = 0; i < K; ++i)
+        if (out->bound[i] < (uint32_t)std::max<int64_t>(P->res_bound[i], 0))
+            return HM_ERR_INVALID_ARGUMENT;
+    if (a->n == 0) return HM_OK;
+    // workspace: arena + degree rows, chunked over values to a memory budget
+    DeviceGuard g(c->device);
+    const uint64_t nslots = P->slots.size();
+    const uint64_t per_value = P->astride * 4 + nslots * 4;
+    size_t freeb = 0, totalb = 0;
+    HM_HIP(c, hipMemGetInfo(&freeb, &totalb));
+    const uint64_t budget = std::max<uint64_t>((uint64_t)(freeb + c->mws_bytes) / 2, 1ull << 28);
+    const uint64_t chunk = std::min<uint64_t>(a->n, budget / per_value);
+    if (chunk == 0) return HM_ERR_UNSUPPORTED;
+    const uint64_t arena_words = ((P->astride * chunk) + 63) & ~(uint64_t)63;
+    HM_HIP(c, grow(c, c->d_mws, c->mws_bytes, (size_t)(arena_words + nslots * chunk) * 4));
+
+    const uint8_t *T = P->d_tab;
+    MulBase B{};
+    B.arena = c->d_mws;
+    B.astride = P->astride;
+    B.deg1 = c->d_mws + arena_words;
+    B.slots = (const MulSlot *)(T + P->off_slots);
+    B.status = c->d_status;
+    const BatchArg oa = batch_arg(out);
+    std::vector<uint32_t> ooff(K);
+    for (uint32_t i = 0, o = 0; i < K; ++i) ooff[i] = o, o += cap_of(out->bound[i]);
+    for (uint64_t e0 = 0; e0 < a->n; e0 += chunk) {
+        B.e0 = e0;
+        B.nv = std::min<uint64_t>(chunk, a->n - e0);
+        HM_HIP(c, hipMemsetAsync(B.deg1, 0, (size_t)nslots * B.nv * 4, c->stream));
+        MulStageArgs S{};
+        S.B = B, S.a = batch_arg(a), S.b = batch_arg(b), S.K = K;
+        fill_bounds(S.ab, a), fill_bounds(S.bb, b);
+        if (launch_mul_stage(S, c->stream)) return hip_fail(c, hipGetLastError());
+        for (uint32_t i = 0; i < K; ++i) {
+            const MulPlan::Col &col = P->cols[i];
+            MulPPArgs pp{};
+            pp.B = B, pp.tasks = (const MulPPTask *)(T + P->off_pp) + col.pp, pp.ntasks = col.npp;
+            if (launch_mul_pp(pp, c->stream)) return hip_fail(c, hipGetLastError());
+            MulScanArgs sc{};
+            sc.B = B;
+            sc.items = (const uint32_t *)(T + P->off_lists) + col.items;
+            sc.prefix = (const uint32_t *)(T + P->off_lists) + col.prefix;
+            sc.nitems = col.nitems;
+            sc.res = col.res;
+            sc.out = oa, sc.out_off = ooff[i], sc.out_cap = cap_of(out->bound[i]);
+            sc.chunks = (std::max(col.maxwords, 2 * sc.out_cap) + 255) / 256;
+            if (launch_mul_scan(sc, c->stream)) return hip_fail(c, hipGetLastError());
+            for (uint32_t q = 0; q < kNW; ++q) {
+                if (!col.ntiles[q]) continue;
+                MulProdArgs pr{};
+                pr.B = B;
+                pr.tasks = (const MulProdTask *)(T + P->off_prod) + col.prod;
+                pr.tiles = (const MulTile *)(T + P->off_tiles) + col.tiles[q];
+                pr.ntiles = col.ntiles[q];
+                if (launch_mul_prod(pr, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
+            }
+        }
+        MulFinalArgs F{};
+        F.B = B, F.res = (const uint32_t *)(T + P->off_res), F.K = K, F.out = oa;
+        fill_bounds(F.ob, out);
+        if (launch_mul_final(F, c->stream)) return hip_fail(c, hipGetLastError());
+    }
+    return HM_OK;
+}
+
+} // namespace hm

@@ -26,7 +26,7 @@ for p in (ROOT, os.path.join(ROOT, "homomorph-rust_amd"), os.path.join(ROOT, "te
     if p not in sys.path:
         sys.path.insert(0, p)
 
-from helpers import as_bytes, bit_ints, fresh_bound, masks, plain  # noqa: E402
+from helpers import as_bytes, bit_ints, fresh_bound, low_bits, masks, plain, digest  # noqa: E402
 from oracle import gf2_model as model  # noqa: E402
 from oracle import oracle_py as oracle  # noqa: E402
 
@@ -42,6 +42,9 @@ CASES = {
     "or_u8_d32": ("or", (32, 8, 8, 8), np.uint8, 2, 108),
     "xor_u8_d32": ("xor", (32, 16, 16, 16), np.uint8, 2, 109),
     "not_u8_d32": ("not", (32, 16, 16, 16), np.uint8, 2, 110),
+    # SURVEY §8(d) configs[3] / row A14: the low 16 result bits of the u32 multiply (the circuit's
+    # columns 0..15), stored as degrees + a SHA-256 per value (the outputs are ~200 KB a value)
+    "mullow16_u32_d128": ("mullow16", (128, 128, 1, 128), np.uint32, 2, 111),
 }
 
 
@@ -98,7 +101,22 @@ def make(name):
                pk_degree=np.asarray(pkdeg, dtype=np.uint32), a_plain=a, b_plain=b,
                a_masks=ma, b_masks=mb, in_bound=bound, a_limbs=la, a_degree=da,
                b_limbs=lb, b_degree=db, op=np.array(op))
-    if op == "encdec":
+    if op.startswith("mullow"):
+        k = int(op[len("mullow"):])
+        l1, d1, b1 = low_bits(la, da, bound, n, k)
+        l2, d2, b2 = low_bits(lb, db, bound, n, k)
+        ob = H.mul_out_bounds(b1, b2)
+        oracle.set_threads(n)
+        lo, do = oracle.mul_batch(l1, d1, b1, l2, d2, b2, k, n, ob)
+        oracle.set_threads(1)
+        dec = oracle.decrypt_batch(sk, lo, do, ob, k, n).reshape(n, k // 8)
+        val = np.zeros(n, dtype=np.uint64)
+        for byte in range(k // 8):
+            val |= dec[:, byte].astype(np.uint64) << np.uint64(8 * byte)
+        out.update(k=np.array(k), out_bound=ob, out_degree=do,
+                   out_sha256=np.array(digest(lo, ob, n)), out_plain=val,
+                   expected_plain=(a.astype(np.uint64) * b.astype(np.uint64)) % (1 << k))
+    elif op == "encdec":
         dec = oracle.decrypt_batch(sk, la, da, bound, nbits, n).view(dtype).reshape(-1)
         out.update(out_bound=bound, out_limbs=la, out_degree=da, out_plain=dec,
                    expected_plain=a)

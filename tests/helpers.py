@@ -60,6 +60,14 @@ def assert_batches_equal(l1, d1, l2, d2, bound, n, what=""):
         raise AssertionError(f"{what}: limb mismatch at {bad.tolist()} (value {bad // stride})")
 
 
+def digest(limbs, bound, n):
+    """Per-value SHA-256 (hex) of a batch's limbs (the batch layout, capacity limbs per bit)."""
+    import hashlib
+    _, _, stride = offsets(bound)
+    l = np.ascontiguousarray(np.asarray(limbs, dtype=np.uint64).reshape(n, stride))
+    return [hashlib.sha256(l[e].astype("<u8").tobytes()).hexdigest() for e in range(n)]
+
+
 def fresh_bound(d, dp, nbits):
     return np.full(nbits, d + dp, dtype=np.uint32)
 
