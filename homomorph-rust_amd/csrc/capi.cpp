@@ -199,7 +199,7 @@ hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n) {
 // =============================================================================================
 extern "C" {
 
-const char *hm_status_string(hm_status s) {
+const char *hm_status_string(int s) { // int: any value a foreign caller passes is defined
     switch (s) {
     case HM_OK: return "ok";
     case HM_ERR_INVALID_PARAMETERS: return "invalid parameters (d < min_d_over_delta * delta)";
@@ -454,6 +454,18 @@ hm_status hm_mul_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, in
     std::vector<int64_t> res;
     if (!mul_result_bounds(L, L, a, b, is_signed != 0, res)) return HM_ERR_UNSUPPORTED;
     for (uint32_t i = 0; i < L; ++i) out[i] = (uint32_t)std::max<int64_t>(res[i], 0);
+    return HM_OK;
+}
+
+hm_status hm_mul_cost(uint32_t L, uint32_t k, const uint32_t *a, const uint32_t *b, int is_signed,
+                      double *word_pairs, double *out_bytes, double *max_degree) {
+    if (!a || !b || L == 0 || L > HM_MAX_BITS || k == 0 || k > L) return HM_ERR_INVALID_ARGUMENT;
+    (void)is_signed; // the signed corners (+1 in column L-1) change no bound
+    double w, o, m;
+    mul_cost_model(L, k, a, b, w, o, m);
+    if (word_pairs) *word_pairs = w;
+    if (out_bytes) *out_bytes = o;
+    if (max_degree) *max_degree = m;
     return HM_OK;
 }
 

@@ -149,5 +149,8 @@ void mul_plans_release(hm_ctx *c);
 // bound exceeds the engine's 2^30 limit.  The same symbolic walk as the plan.
 bool mul_result_bounds(uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,
                        bool is_signed, std::vector<int64_t> &res);
+// The same walk over bounds only, without limits: word-pair products, output bytes, max degree.
+void mul_cost_model(uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,
+                    double &pairs, double &out_bytes, double &maxdeg);
 
 } // namespace hm

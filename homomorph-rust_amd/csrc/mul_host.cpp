@@ -13,6 +13,7 @@
 // identity and a product with null is null, so dropping them changes no output bit.
 // Plans (with their device task tables) are cached per context, keyed by the operand bounds.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <memory>
 
@@ -248,6 +249,33 @@ bool mul_result_bounds(uint32_t nbits, uint32_t K, const uint32_t *a, const uint
     if (!build_plan(P)) return false;
     res = P.res_bound;
     return true;
+}
+
+// The plan's recursion over bounds only (no slots, no limits): the cost model of hm_mul_cost.
+void mul_cost_model(uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,
+                    double &pairs, double &out_bytes, double &maxdeg) {
+    (void)nbits;
+    std::vector<double> prev, cur;
+    pairs = 0, out_bytes = 0, maxdeg = 0;
+    for (uint32_t i = 0; i < K; ++i) {
+        std::vector<double> items;
+        for (uint32_t j = 0; j <= i; ++j) items.push_back((double)a[j] + (double)b[i - j]);
+        items.insert(items.end(), prev.begin(), prev.end());
+        const bool push = i + 1 < K;
+        cur.clear();
+        double pb = -1;
+        for (double x : items) {
+            if (push && pb >= 0) {
+                pairs += (std::floor(pb / 32) + 1) * (std::floor(x / 32) + 1);
+                cur.push_back(pb + x);
+                maxdeg = std::max(maxdeg, pb + x);
+            }
+            pb = std::max(pb, x);
+            maxdeg = std::max(maxdeg, pb);
+        }
+        out_bytes += 8 * (std::floor(std::max(pb, 0.0) / 64) + 1);
+        prev.swap(cur);
+    }
 }
 
 void mul_plans_release(hm_ctx *c) {

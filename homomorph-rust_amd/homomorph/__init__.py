@@ -208,6 +208,28 @@ def mul_out_bounds(a_bound, b_bound, signed=False) -> np.ndarray:
     return out
 
 
+def mul_cost(a_bound, b_bound, k=None, signed=False) -> dict:
+    """hm_mul_cost: the planner's price of the low k output bits of the carry-save multiplier
+    (all bits when k is None) -- word_pairs (32x32 carry-less word products), out_bytes,
+    max_degree.  Host only; works for circuits far beyond what any device can run."""
+    a, b = _u32(a_bound), _u32(b_bound)
+    k = a.size if k is None else int(k)
+    w, o, m = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    _check(lib().hm_mul_cost(a.size, k, _p32(a), _p32(b), int(signed), ctypes.byref(w),
+                             ctypes.byref(o), ctypes.byref(m)), "hm_mul_cost")
+    return {"word_pairs": w.value, "out_bytes": o.value, "max_degree": m.value}
+
+
+def wire_info(data: bytes) -> dict:
+    """hm_wire_peek: {"nbits", "n", "bound"} of a wire image (host only)."""
+    nb, n = ctypes.c_uint32(), ctypes.c_uint64()
+    bound = np.zeros(_lib.HM_MAX_BITS, dtype=np.uint32)
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    _check(lib().hm_wire_peek(buf, len(data), ctypes.byref(nb), ctypes.byref(n), _p32(bound)),
+           "hm_wire_peek")
+    return {"nbits": nb.value, "n": n.value, "bound": bound[: nb.value].copy()}
+
+
 def gate_out_bounds(op, a_bound, b_bound=None) -> np.ndarray:
     a = _u32(a_bound)
     b = _u32(b_bound) if b_bound is not None else None
@@ -286,6 +308,27 @@ class Ciphered:
 
     def nbytes(self) -> int:
         return self.stride * 8 * self.n
+
+    def to_wire(self, ctx: "Context") -> bytes:
+        """The batch's wire image (include/homomorph_gpu.h "wire format"; synchronous)."""
+        size = int(lib().hm_wire_bytes(self.nbits, _p32(self.bound), self.n))
+        if size == 0:
+            raise EngineError(_lib.ERR_UNSUPPORTED, "to_wire")
+        buf = (ctypes.c_uint8 * size)()
+        c = self._c()
+        _check(lib().hm_wire_encode(ctx._h, ctypes.byref(c), buf, size), "hm_wire_encode")
+        return bytes(buf)
+
+    @classmethod
+    def from_wire(cls, ctx: "Context", data: bytes, plain_dtype=None) -> "Ciphered":
+        """A device batch from a wire image (validated on the host: HM_ERR_BAD_INPUT)."""
+        info = wire_info(data)
+        out = cls.empty(info["n"], info["bound"], ctx.device, plain_dtype)
+        c = out._c()
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        ctx._launch(lambda: lib().hm_wire_decode(ctx._h, buf, len(data), ctypes.byref(c)),
+                    "hm_wire_decode")
+        return out
 
 
 class Polys:
@@ -517,6 +560,13 @@ class Context:
 
     # ---- operations (Context::apply1 / apply2, src/context.rs:496-527)
     def validate_operation(self, op) -> None:
+        """Context::validate_operation (src/context.rs:310-323).  Built-in operations ask the
+        engine (hm_validate_operation); a user operation supplies MIN_D_OVER_DELTA itself."""
+        if not hasattr(op, "CODE"):
+            req = int(op.MIN_D_OVER_DELTA)
+            if self._params.d < req * self._params.delta:
+                raise OperationError(req, self._params.d, self._params.delta)
+            return
         req = ctypes.c_uint16()
         st = lib().hm_validate_operation(self._h, op.CODE, ctypes.byref(req))
         if st == _lib.ERR_INVALID_PARAMETERS:
@@ -564,14 +614,24 @@ class Context:
         return out
 
     def apply1(self, op, a: Ciphered) -> Ciphered:
-        """HomomorphicOperation1 (the reference mutates in place; the batch returns a new value)."""
+        """Context::apply1 (src/context.rs:496-510): validate, then HomomorphicOperation1::apply
+        on `&mut a` -- IN PLACE, as the reference mutates its argument (the NOT gate keeps every
+        bound, so the kernel writes each bit over the one it read).  Returns `a` itself."""
         self.validate_operation(op)
         need = gate_out_bounds(op, a.bound)
-        out = Ciphered.empty(a.n, need, self.device, a.plain_dtype)
-        ca, co = a._c(), out._c()
+        if not np.array_equal(need, a.bound):
+            raise ValueError(f"{op.__name__} changes the bounds: not an in-place operation")
+        ca = a._c()
         self._launch(lambda: lib().hm_gate_batch(self._h, op.CODE, ctypes.byref(ca), None,
-                                                 ctypes.byref(co)), op.__name__)
-        return out
+                                                 ctypes.byref(ca)), op.__name__)
+        return a
+
+    def apply_n(self, op, args) -> Ciphered:
+        """Context::apply_n (src/context.rs:535-546): validate `op`'s MIN_D_OVER_DELTA, then call
+        the user operation `op.apply(ctx, args)` (HomomorphicOperation<N>, operations.rs:204-213:
+        the crate ships no N-ary operation of its own; a user op composes the batched ones)."""
+        self.validate_operation(op)
+        return op.apply(self, list(args))
 
     # ---- polynomial primitives
     def poly_add(self, a: Polys, b: Polys) -> Polys:
@@ -643,3 +703,19 @@ def value_slice(c: Ciphered, lo: int, hi: int) -> Ciphered:
     s = c.stride
     return Ciphered(c.limbs[lo * s: hi * s], c.degree[lo:hi], c.bound, c.nbits, hi - lo,
                     c.plain_dtype)
+
+
+def pad_bits(c: Ciphered, nbits: int) -> Ciphered:
+    """A copy of c widened to nbits ciphertext bits per value, the new bits null polynomials
+    (bound 0, one zero limb): e.g. a k-bit product decrypted as a 16-bit value."""
+    torch = _torch()
+    extra = int(nbits) - c.nbits
+    if extra < 0:
+        raise ValueError("pad_bits only widens")
+    limbs = torch.cat([c.limbs.view(c.n, c.stride),
+                       torch.zeros((c.n, extra), dtype=c.limbs.dtype, device=c.limbs.device)],
+                      dim=1).reshape(-1)
+    deg = torch.cat([c.degree.view(c.n, c.nbits),
+                     torch.zeros((c.n, extra), dtype=c.degree.dtype, device=c.degree.device)], dim=1)
+    bound = np.concatenate([c.bound, np.zeros(extra, dtype=np.uint32)])
+    return Ciphered(limbs, deg, bound, nbits, c.n, c.plain_dtype)

@@ -73,6 +73,9 @@ SIGNATURES = {
     "hm_fresh_bound": (ctypes.c_uint32, [vp]),
     "hm_add_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, u32p]),
     "hm_mul_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, ctypes.c_int, u32p]),
+    "hm_mul_cost": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double)]),
     "hm_gate_out_bounds": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, u32p, u32p, u32p]),
     "hm_batch_stride": (ctypes.c_uint64, [ctypes.c_uint32, u32p]),
     "hm_encrypt_batch": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.POINTER(HmBatch)]),
@@ -87,6 +90,11 @@ SIGNATURES = {
     "hm_poly_mul_batch": (ctypes.c_int, [vp] + [ctypes.POINTER(HmPolys)] * 3),
     "hm_poly_rem_batch": (ctypes.c_int, [vp, ctypes.POINTER(HmPolys), u64p, ctypes.c_size_t,
                                          ctypes.POINTER(HmPolys)]),
+    "hm_wire_bytes": (ctypes.c_uint64, [ctypes.c_uint32, u32p, ctypes.c_uint64]),
+    "hm_wire_peek": (ctypes.c_int, [vp, ctypes.c_size_t, u32p, ctypes.POINTER(ctypes.c_uint64),
+                                    u32p]),
+    "hm_wire_encode": (ctypes.c_int, [vp, ctypes.POINTER(HmBatch), vp, ctypes.c_size_t]),
+    "hm_wire_decode": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.POINTER(HmBatch)]),
     "hm_ctx_synchronize": (ctypes.c_int, [vp]),
 }
 

@@ -94,7 +94,8 @@ typedef struct hm_polys {
 } hm_polys;
 
 /* ---------------- library / context ---------------- */
-const char *hm_status_string(hm_status s);
+/* Text of a status code; any int is accepted ("unknown status" outside hm_status). */
+const char *hm_status_string(int s);
 uint32_t hm_abi_version(void);
 
 /* Context::new(Parameters::new(d, dp, delta, tau)) — src/context.rs:345-351 with the asserts of
@@ -164,6 +165,15 @@ hm_status hm_add_out_bounds(uint32_t nbits, const uint32_t *a_bound, const uint3
 /* Output bounds of the carry-save multiplier (common.rs:66-105 / :115-155). */
 hm_status hm_mul_out_bounds(uint32_t nbits, const uint32_t *a_bound, const uint32_t *b_bound,
                             int is_signed, uint32_t *out_bound);
+/* Cost model of the low k output bits of the nbits-bit carry-save multiplier (host only, no device
+ * work): the symbolic run of common.rs:66-105 over static degree bounds, exactly as
+ * hm_mul_low_batch plans it but without the engine's size limits, so the full u32 circuit (which
+ * no engine can run: SURVEY.md s0.6) can be priced.  word_pairs: 32x32-bit carry-less word
+ * products over all carries p_t * x_t; out_bytes: the k output bits at their capacities;
+ * max_degree: the largest degree bound of any polynomial the circuit builds.  Outputs may be
+ * NULL. */
+hm_status hm_mul_cost(uint32_t nbits, uint32_t k, const uint32_t *a_bound, const uint32_t *b_bound,
+                      int is_signed, double *word_pairs, double *out_bytes, double *max_degree);
 /* Output bounds of a gate (common.rs:5-35). */
 hm_status hm_gate_out_bounds(hm_op gate, uint32_t nbits, const uint32_t *a_bound,
                              const uint32_t *b_bound, uint32_t *out_bound);
@@ -222,6 +232,30 @@ hm_status hm_poly_mul_batch(hm_ctx *ctx, const hm_polys *a, const hm_polys *b, h
  * polynomial of a; s = 0 -> HM_ERR_DIVIDE_BY_ZERO, s = 1 -> HM_ERR_DIVISOR_IS_ONE. */
 hm_status hm_poly_rem_batch(hm_ctx *ctx, const hm_polys *a, const uint64_t *s_limbs,
                             size_t s_nlimbs, hm_polys *out);
+
+/* ---------------- ciphertext batch wire format ---------------- */
+/* The reference serialises no ciphertexts (only keys, src/context.rs:153-194, :239-297); this is
+ * the engine's storage / transfer format for a batch, all fields little-endian:
+ *   offset 0   magic "HMCB" (4 bytes)      offset 4   version (u32) = 1
+ *   offset 8   nbits (u32)                 offset 12  flags (u32) = 0
+ *   offset 16  n (u64)                     offset 24  bound[nbits] (u32)
+ *   then       degree[n*nbits] (u32), zero padding to a multiple of 8 bytes,
+ *   then       limbs[n*stride] (u64) in the batch layout above (stride = hm_batch_stride).
+ * One Ciphered<T> is n = 1 with its Vec<CipheredBit> as the nbits polynomials, bit k of the
+ * bincode image first-to-last (src/cipher.rs:127-130, :253-259).  Size in bytes of a batch: */
+uint64_t hm_wire_bytes(uint32_t nbits, const uint32_t *bound, uint64_t n);
+/* Parse a header (host buffer of len bytes): nbits, n and, when bound is non-NULL, the nbits
+ * bounds.  HM_ERR_INVALID_ARGUMENT for a bad magic / version / flags or a length that disagrees
+ * with the header. */
+hm_status hm_wire_peek(const uint8_t *src, size_t len, uint32_t *nbits, uint64_t *n,
+                       uint32_t *bound);
+/* Device batch -> host wire image (synchronous: waits for the context's stream).  cap: bytes at
+ * dst, at least hm_wire_bytes(in). */
+hm_status hm_wire_encode(hm_ctx *ctx, const hm_batch *in, uint8_t *dst, size_t cap);
+/* Host wire image -> device batch `out` (caller-allocated from hm_wire_peek: same nbits, n and
+ * bounds).  Every polynomial is validated on the host first (degree within its bound, its top
+ * coefficient set, zeros above it) -> HM_ERR_BAD_INPUT; synchronous. */
+hm_status hm_wire_decode(hm_ctx *ctx, const uint8_t *src, size_t len, hm_batch *out);
 
 /* ---------------- status / sync ---------------- */
 /* Waits for the context's stream, then returns (and clears) the first device-side error raised by

@@ -124,9 +124,19 @@ def seeded_chacha(seed):
     return key, nonce
 
 
-def seeded_random_bytes(seed, draw, n):
-    """Bytes of the `draw`-th (0-based) hm_random_bytes call of size n after seeding."""
+def seeded_random_bytes(seed, draw, n, start=0):
+    """Bytes [start, start+n) of the `draw`-th (0-based) hm_random_bytes call after seeding."""
     key, nonce = seeded_chacha(seed)
     nonce = (nonce + draw) & (2**64 - 1)
-    blocks = [chacha20_block(key, c, nonce) for c in range((n + 63) // 64)]
-    return np.frombuffer(b"".join(blocks)[:n], dtype=np.uint8)
+    c0, c1 = start // 64, (start + n + 63) // 64
+    blocks = b"".join(chacha20_block(key, c, nonce) for c in range(c0, c1))
+    return np.frombuffer(blocks[start - 64 * c0: start - 64 * c0 + n], dtype=np.uint8)
+
+
+def seeded_value_masks(seed, draw, idx, nbits, mask_bytes):
+    """Masks the engine drew for values idx in its `draw`-th CSPRNG draw of an encrypt call
+    (masks=None): value e's nbits*mask_bytes bytes start at e*nbits*mask_bytes.  Returns
+    (len(idx), nbits, mask_bytes) uint8 -- only the ChaCha20 blocks of those values are made."""
+    per = nbits * mask_bytes
+    return np.stack([seeded_random_bytes(seed, draw, per, int(e) * per).reshape(nbits, mask_bytes)
+                     for e in idx])

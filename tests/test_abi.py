@@ -94,6 +94,53 @@ def test_mul_and_gate_bounds_cover_model(oracle):
         assert np.all(np.asarray(do).reshape(3, 8) <= gb[None, :])
 
 
+def test_mul_cost_matches_survey_appendix_a3():
+    """hm_mul_cost prices the carry-save circuit from its static bounds (SURVEY.md Appendix A.3:
+    top-bit degree per K; the full u32 circuit ~4.7e17 limb-clmuls = 1.9e18 word pairs and
+    ~8.4 GiB of output bits), and agrees with hm_mul_out_bounds where both apply."""
+    import homomorph as H
+    b = np.full(32, 256, np.uint32)
+    top = {8: 14336, 12: 146432, 16: 1.6e6, 20: 1.9e7, 32: 3.4e10}
+    prev = 0
+    for k, deg in top.items():
+        c = H.mul_cost(b, b, k)
+        assert abs(c["max_degree"] - deg) / deg < 0.05, (k, c)
+        assert c["word_pairs"] > prev
+        prev = c["word_pairs"]
+    full = H.mul_cost(b, b)
+    assert 1.8e18 < full["word_pairs"] < 2.0e18 and 8.0 * 2**30 < full["out_bytes"] < 8.8 * 2**30
+    ob = H.mul_out_bounds(b[:8], b[:8])
+    assert H.mul_cost(b[:8], b[:8])["out_bytes"] == 8 * H.batch_stride(ob)
+
+
+def test_wire_header_host_only():
+    """The wire format's header (include/homomorph_gpu.h): a hand-built image parses, and bad
+    magic / version / flags / length are rejected -- host-only entry points, no GPU."""
+    import homomorph as H
+    bound = np.array([128, 300, 0], np.uint32)
+    n = 2
+    stride = int((bound // 64 + 1).sum())
+    size = H.lib().hm_wire_bytes(3, H._p32(bound), n)
+    doff = 24 + 4 * 3
+    loff = (doff + 4 * n * 3 + 7) // 8 * 8
+    assert size == loff + 8 * n * stride
+    img = bytearray(size)
+    img[:4] = b"HMCB"
+    img[4:8] = (1).to_bytes(4, "little")
+    img[8:12] = (3).to_bytes(4, "little")
+    img[16:24] = n.to_bytes(8, "little")
+    img[24:doff] = bound.astype("<u4").tobytes()
+    info = H.wire_info(bytes(img))
+    assert info["nbits"] == 3 and info["n"] == n and np.array_equal(info["bound"], bound)
+    for off, val in ((0, b"XMCB"), (4, (2).to_bytes(4, "little")), (12, (1).to_bytes(4, "little"))):
+        bad = bytearray(img)
+        bad[off:off + len(val)] = val
+        with pytest.raises(H.EngineError):
+            H.wire_info(bytes(bad))
+    with pytest.raises(H.EngineError):
+        H.wire_info(bytes(img[:-1]))
+
+
 def test_invalid_bounds_rejected(L):
     from homomorph import _lib
     a = np.full(4, 10, np.uint32)

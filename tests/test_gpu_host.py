@@ -129,3 +129,44 @@ def test_graph_refuses_replay_after_buffer_change(H):
     g2.replay()
     ctx.synchronize()
     assert np.array_equal(ctx.decrypt(out), 2 * np.arange(8, dtype=np.uint32))
+
+
+def test_apply1_is_in_place_and_apply_n_runs_user_ops(H, oracle):
+    """Context::apply1 mutates its argument (src/context.rs:496-510: `a: &mut Ciphered<T>`):
+    NOT runs with out == a and the result equals the oracle's.  Context::apply_n validates the
+    user operation's requirement and calls it (operations.rs:204-213; the doc example's N-ary
+    op on [&a, &b]), here a 3-ary sum composed of the batched additions."""
+    params = (64, 64, 1, 64)
+    ctx = H.Context(H.Parameters(*params))
+    ctx.seed_rng(8)
+    ctx.generate_secret_key()
+    ctx.generate_public_key()
+    x = plain(40, np.uint16, 1)
+    m = masks(40, 16, 64, 2)
+    c = ctx.encrypt(x, masks=m)
+    ptr = c.limbs.data_ptr()
+    assert ctx.apply1(H.HomomorphicNotGate, c) is c and c.limbs.data_ptr() == ptr
+    pk = ctx.get_public_key().limbs
+    la, da = oracle.encrypt_batch(pk, as_bytes(x), m, c.bound)
+    rl, rd = oracle.gate_batch("not", la, da, c.bound, la, da, c.bound, 16, 40, c.bound)
+    gl, gd = c.to_host()
+    assert_batches_equal(gl, gd, rl, rd, c.bound, 40, "in-place not")
+    assert np.array_equal(ctx.decrypt(c), ~x)
+
+    class Sum3:  # a user HomomorphicOperation<3, u16> (+ OperationRequirement)
+        MIN_D_OVER_DELTA = 21
+
+        @staticmethod
+        def apply(cx, args):
+            a, b, d = args
+            return cx.apply2(H.HomomorphicAddition, cx.apply2(H.HomomorphicAddition, a, b), d)
+
+    y, z = plain(40, np.uint16, 3), plain(40, np.uint16, 4)
+    s = ctx.apply_n(Sum3, [ctx.encrypt(x), ctx.encrypt(y), ctx.encrypt(z)])
+    assert np.mean(ctx.decrypt(s) == (x + y + z).astype(np.uint16)) > 0.9
+
+    class Needy(Sum3):
+        MIN_D_OVER_DELTA = 1000
+
+    with pytest.raises(H.OperationError):
+        ctx.apply_n(Needy, [c, c, c])

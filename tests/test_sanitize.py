@@ -1,0 +1,44 @@
+"""SURVEY.md s5 "race detection / sanitizers": ASan + UBSan builds of the CPU oracle and of the
+engine library's host code, run on the CPU (GPU sanitizers are not available on this pool).
+
+- tests/sanitize/oracle_san.c: the reference's polynomial KATs and an encrypt -> add / mul /
+  gates -> decrypt round trip through oracle/homomorph_oracle.c;
+- tests/sanitize/capi_san.cpp: every host-only C-ABI entry point (status strings, bounds, the
+  multiplier cost model, strides, the wire-format parser under 20k corrupted headers, NULL
+  contexts), with the device kernels linked in unsanitised.
+Any sanitizer report aborts the binary (-fno-sanitize-recover=all) and fails the test.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAN = os.path.join(ROOT, "tests", "sanitize")
+
+
+@pytest.fixture(scope="module")
+def built():
+    if shutil.which("gcc") is None or not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("needs gcc and hipcc")
+    eng = os.path.join(ROOT, "homomorph-rust_amd")
+    subprocess.run(["make", "-s", "-C", eng], check=True, timeout=1200)
+    subprocess.run(["make", "-s", "-j4", "-C", SAN], check=True, timeout=1200)
+    return os.path.join(SAN, "_build")
+
+
+def _run(path):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([path], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return r.stdout
+
+
+def test_oracle_under_asan_ubsan(built):
+    assert "ok" in _run(os.path.join(built, "oracle_san"))
+
+
+def test_engine_host_code_under_asan_ubsan(built):
+    assert "ok" in _run(os.path.join(built, "capi_san"))
