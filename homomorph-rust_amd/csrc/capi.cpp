@@ -402,6 +402,13 @@ hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, ui
     return HM_OK;
 }
 
+hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) {
+    if (!c || (ka_min && (ka_leaf < 32 || ka_leaf > 384))) return HM_ERR_INVALID_ARGUMENT;
+    c->ka_min = ka_min;
+    c->ka_leaf = ka_leaf & ~31u;
+    return HM_OK;
+}
+
 hm_status hm_validate_operation(const hm_ctx *c, hm_op op, uint16_t *req) {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     const uint16_t m = min_d_over_delta(op);

@@ -61,6 +61,9 @@ struct hm_ctx {
     uint64_t generation = 0;
     // column multiplier plans (device task tables), keyed by the operand bounds; see mul_host.cpp
     std::vector<hm::MulPlan *> mul_plans; // owned; freed by mul_plans_release
+    // Karatsuba carry products (hm_ctx_set_mul_options): shorter operand >= ka_min words (0 =
+    // never), recursion down to leaves of at most ka_leaf words
+    uint32_t ka_min = 1024, ka_leaf = 256;
 };
 
 namespace hm {

@@ -144,6 +144,47 @@ struct MulProdArgs {
     const MulTile *tiles;
     uint32_t ntiles;
 };
+// Karatsuba products (mul_host.cpp "Karatsuba"): the big carries p_t * x_t of the deep columns
+// run as a recursion over arena VIEWS (u32-word ranges of a value's arena; words past `valid`
+// read as zero).  Level by level: sums of halves (KaSum), leaf products (MulVTask, schoolbook
+// tiles), and recombination R = z0 + (z0 + z1 + z2) X^h + z1 X^2h (KaComb).
+struct KaSum {
+    uint32_t src, valid; // operand view (arena words)
+    uint32_t dst;        // dst[0:h) = src[0:h) ^ src[h:2h)
+};
+struct KaSumArgs {
+    MulBase B;
+    const KaSum *t;
+    uint32_t nt, h;
+};
+struct MulVTask {
+    uint32_t u, nu, v, nv; // operand views (nu, nv valid words; 0 = null)
+    uint32_t out, nout;    // out[0:nout) = U * V
+};
+struct MulVTile {
+    uint32_t task, base;
+};
+struct MulVProdArgs {
+    MulBase B;
+    const MulVTask *tasks;
+    const MulVTile *tiles;
+    uint32_t ntiles;
+};
+constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
+struct KaComb {
+    uint32_t z0, z1, z2; // child results, 2h words each (z1 may be kKaNone)
+    uint32_t r, rcap;    // parent result: r[0:min(4h, rcap))
+};
+struct KaCombArgs {
+    MulBase B;
+    const KaComb *t;
+    uint32_t nt, h;
+};
+struct MulDegArgs { // deg1[out] of an exact product from its operands' deg1 (null -> 0)
+    MulBase B;
+    uint32_t u, v, out;
+};
+
 struct MulFinalArgs {
     MulBase B;
     const uint32_t *res; // K degree slots of the output bits
@@ -186,6 +227,10 @@ int launch_mul_pp(const MulPPArgs &a, void *stream);
 int launch_mul_scan(const MulScanArgs &a, void *stream);
 int launch_mul_prod(const MulProdArgs &a, uint32_t w, void *stream);
 int launch_mul_final(const MulFinalArgs &a, void *stream);
+int launch_ka_sum(const KaSumArgs &a, void *stream);
+int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
+int launch_ka_comb(const KaCombArgs &a, void *stream);
+int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches
 int launch_poly_add(const PolyArgs &a, void *stream);
 int launch_poly_mul(const PolyArgs &a, void *stream);

@@ -220,6 +220,128 @@ int launch_mul_prod(const MulProdArgs &P, uint32_t w, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Karatsuba over arena views (mul_host.cpp "Karatsuba").  All offsets and h are multiples of 4
+// words, so every access is a whole uint4; one wave per (value, task, 256-word chunk).
+
+// dst[0:h) = src[0:h) ^ src[h:2h), words at or past `valid` of src read as zero
+__global__ void __launch_bounds__(256) ka_sum_kernel(KaSumArgs A) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint32_t chunks = (A.h + 255) / 256;
+    const uint64_t per_value = (uint64_t)A.nt * chunks;
+    const uint64_t e = g / per_value;
+    if (e >= A.B.nv) return;
+    const uint32_t r = (uint32_t)(g % per_value);
+    const KaSum t = A.t[r / chunks];
+    const uint32_t w = (r % chunks) * 256 + 4u * (uint32_t)lane_id();
+    if (w >= A.h) return;
+    const uint32_t *base = A.B.arena + e * A.B.astride;
+    uint4 lo = make_uint4(0u, 0u, 0u, 0u), hi = lo;
+    if (w < t.valid) lo = *(const uint4 *)(base + t.src + w);
+    if (A.h + w < t.valid) hi = *(const uint4 *)(base + t.src + A.h + w);
+    *(uint4 *)(A.B.arena + e * A.B.astride + t.dst + w) =
+        make_uint4(lo.x ^ hi.x, lo.y ^ hi.y, lo.z ^ hi.z, lo.w ^ hi.w);
+}
+
+int launch_ka_sum(const KaSumArgs &A, void *stream) {
+    const uint64_t waves = A.B.nv * A.nt * ((A.h + 255) / 256);
+    if (!waves) return 0;
+    hipLaunchKernelGGL(ka_sum_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// leaf products over views: one wave per (value, 64*W-word output tile), as mul_prod_kernel
+template <int W>
+__global__ void __launch_bounds__(256) mul_vprod_kernel(MulVProdArgs P) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint64_t e = g / P.ntiles;
+    const uint32_t k = (uint32_t)(g % P.ntiles);
+    if (e >= P.B.nv) return;
+    const MulVTile tl = P.tiles[k];
+    const MulVTask T = P.tasks[tl.task];
+    uint32_t *arena = P.B.arena + e * P.B.astride;
+    uint32_t *O = arena + T.out;
+    const int nout = (int)rfl(T.nout), base = (int)rfl(tl.base);
+    const int nu = (int)rfl(T.nu), nv = (int)rfl(T.nv);
+    if (nu == 0 || nv == 0) {
+        for (int j = 0; j < W; ++j) {
+            const int w = base + lane_id() * W + j;
+            if (w < nout) O[w] = 0u;
+        }
+        return;
+    }
+    const uint32_t *U = arena + T.u, *V = arena + T.v;
+    if (base == 0)
+        mul_tile<W, kMulQC, false, pair_mode<W>(), false>(U, nu, V, nv, nullptr, 0, O, nout, 0);
+    else
+        mul_tile<W, kMulQC, true, pair_mode<W>(), false>(U, nu, V, nv, nullptr, 0, O, nout, base);
+}
+
+int launch_mul_vprod(const MulVProdArgs &P, uint32_t w, void *stream) {
+    const uint64_t waves = P.B.nv * P.ntiles;
+    if (!waves) return 0;
+    const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+    switch (w) {
+    case 1: hipLaunchKernelGGL(mul_vprod_kernel<1>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 2: hipLaunchKernelGGL(mul_vprod_kernel<2>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 4: hipLaunchKernelGGL(mul_vprod_kernel<4>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 8: hipLaunchKernelGGL(mul_vprod_kernel<8>, grid, block, 0, (hipStream_t)stream, P); break;
+    case 12: hipLaunchKernelGGL(mul_vprod_kernel<12>, grid, block, 0, (hipStream_t)stream, P); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// r[0:min(4h, rcap)) = z0 + (z0 + z1 + z2) X^h + z1 X^2h  (z* are 2h words; X^h = h words)
+__global__ void __launch_bounds__(256) ka_comb_kernel(KaCombArgs A) {
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
+    const uint32_t h = A.h, chunks = (4 * h + 255) / 256;
+    const uint64_t per_value = (uint64_t)A.nt * chunks;
+    const uint64_t e = g / per_value;
+    if (e >= A.B.nv) return;
+    const uint32_t r = (uint32_t)(g % per_value);
+    const KaComb t = A.t[r / chunks];
+    const uint32_t w = (r % chunks) * 256 + 4u * (uint32_t)lane_id();
+    if (w >= 4 * h || w >= t.rcap) return;
+    uint32_t *base = A.B.arena + e * A.B.astride;
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    auto ld = [&](uint32_t off, uint32_t i) -> uint4 {
+        return off == kKaNone ? zero : *(const uint4 *)(base + off + i);
+    };
+    auto x = [](uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); };
+    const uint32_t seg = w / h, o = w % h;
+    uint4 v;
+    if (seg == 0) v = ld(t.z0, o);
+    else if (seg == 1) v = x(x(ld(t.z0, h + o), ld(t.z0, o)), x(ld(t.z1, o), ld(t.z2, o)));
+    else if (seg == 2) v = x(x(ld(t.z1, o), ld(t.z0, h + o)), x(ld(t.z1, h + o), ld(t.z2, h + o)));
+    else v = ld(t.z1, h + o);
+    *(uint4 *)(base + t.r + w) = v;
+}
+
+int launch_ka_comb(const KaCombArgs &A, void *stream) {
+    const uint64_t waves = A.B.nv * A.nt * ((4 * A.h + 255) / 256);
+    if (!waves) return 0;
+    hipLaunchKernelGGL(ka_comb_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// deg(u*v) = deg u + deg v exactly (GF(2)[X] has no zero divisors); null if either is null
+__global__ void __launch_bounds__(256) mul_deg_kernel(MulDegArgs A) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= A.B.nv) return;
+    const uint32_t du = A.B.deg1[(uint64_t)A.u * A.B.nv + e], dv = A.B.deg1[(uint64_t)A.v * A.B.nv + e];
+    A.B.deg1[(uint64_t)A.out * A.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+}
+
+int launch_mul_deg(const MulDegArgs &A, void *stream) {
+    if (!A.B.nv) return 0;
+    hipLaunchKernelGGL(mul_deg_kernel, dim3((unsigned)((A.B.nv + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // output degree words (exact; null -> 0) and the capacity check
 __global__ void __launch_bounds__(256) mul_final_kernel(MulFinalArgs F) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

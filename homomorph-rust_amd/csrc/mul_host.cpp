@@ -13,6 +13,7 @@
 // identity and a product with null is null, so dropping them changes no output bit.
 // Plans (with their device task tables) are cached per context, keyed by the operand bounds.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -37,10 +38,20 @@ inline bool pp_flip(bool is_signed, uint32_t L, uint32_t i, uint32_t j) {
 
 } // namespace
 
+// One Karatsuba product (see "Karatsuba" below): its launches, in order.
+struct KaProg {
+    uint32_t u, v, out;                          // slots (exact degrees: deg1)
+    std::vector<std::array<uint32_t, 3>> sums;   // per level 1..k: (first KaSum, count, h)
+    uint32_t vtask = 0, nvtask = 0;              // leaf products (MulVTask range)
+    uint32_t tiles[kNW] = {}, ntiles[kNW] = {};  // their tiles (MulVTile ranges) per width class
+    std::vector<std::array<uint32_t, 3>> combs;  // per level k..1: (first KaComb, count, h)
+};
+
 struct MulPlan {
     // key
     uint32_t L = 0, K = 0;
     bool is_signed = false;
+    uint32_t ka_min = 0, ka_leaf = 0;           // Karatsuba options (hm_ctx_set_mul_options)
     std::vector<uint32_t> ab, bb;
     // geometry
     std::vector<MulSlot> slots;
@@ -54,6 +65,7 @@ struct MulPlan {
         uint32_t maxwords;         // widest prefix / result
         uint32_t prod;             // MulProdTask offset (in tasks)
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
+        std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
     std::vector<uint32_t> res_slots;
@@ -62,9 +74,14 @@ struct MulPlan {
     std::vector<uint32_t> lists;
     std::vector<MulProdTask> prod;
     std::vector<MulTile> tiles;
+    std::vector<KaSum> ka_sums;
+    std::vector<MulVTask> ka_vtasks;
+    std::vector<MulVTile> ka_vtiles;
+    std::vector<KaComb> ka_combs;
     uint8_t *d_tab = nullptr;
     size_t tab_bytes = 0;
     size_t off_slots = 0, off_pp = 0, off_lists = 0, off_prod = 0, off_tiles = 0, off_res = 0;
+    size_t off_ka_sums = 0, off_ka_vtasks = 0, off_ka_vtiles = 0, off_ka_combs = 0;
     uint64_t work = 0; // word-pair products (statistics)
 };
 
@@ -75,11 +92,88 @@ struct Region {
     uint64_t base = 0;
 };
 
+// ---------------------------------------------------------------------------------------------
+// Karatsuba.  A carry product u * v whose shorter operand has at least ka_min words is computed
+// as a Karatsuba recursion instead of schoolbook tiles: operands padded to N = leaf * 2^k words
+// split into halves lo/hi, the three half-size products z0 = lo_u lo_v, z1 = hi_u hi_v,
+// z2 = (lo_u + hi_u)(lo_v + hi_v), and u v = z0 + (z0 + z1 + z2) X^h + z1 X^2h (h = half size).
+// Exact over GF(2)[X] (the same polynomial as the reference's bit-serial product,
+// polynomial.rs:252-310), 3^k leaf products of leaf x leaf words instead of 4^k.  Every node is
+// static (slot capacities are static), so the whole recursion is planned here: views into the
+// arena, sums and child results in a scratch region (KA) reused product after product.  A
+// subtree whose high halves are all padding (zero) is dropped: z1 = 0.
+namespace {
+
+// Views while planning: (region << 28) | word offset relative to the region (regions are placed
+// after the symbolic run); kKaNone stays as is.
+constexpr uint32_t kRegShift = 28, kRelMask = (1u << kRegShift) - 1;
+
+struct KaBuild {
+    uint32_t ka_region, leaf;
+    uint64_t top = 0, max = 0; // scratch bump allocator in the KA region (words)
+    std::vector<std::vector<KaSum>> sums;   // by split depth
+    std::vector<std::vector<KaComb>> combs; // by split depth
+    std::vector<MulVTask> leaves;
+
+    uint32_t alloc(uint64_t words) {
+        const uint64_t o = top;
+        top += (words + 3) & ~(uint64_t)3;
+        max = std::max(max, top);
+        return (ka_region << kRegShift) | (uint32_t)o;
+    }
+    // r[0:min(2n, rcap)) = U * V for views u (un valid words), v (vn), both of logical size n
+    void node(uint32_t lvl, uint32_t uo, uint32_t un, uint32_t vo, uint32_t vn, uint32_t n,
+              uint32_t r, uint32_t rcap) {
+        if (n == leaf) {
+            leaves.push_back({uo, std::min(un, n), vo, std::min(vn, n), r, std::min(2 * n, rcap)});
+            return;
+        }
+        const uint32_t h = n / 2;
+        if (un <= h && vn <= h) {
+            // both high halves are padding: u v = lo_u lo_v (one child, not three); the
+            // recombination with z2 = z0, z1 = 0 copies it and zero-fills r above it
+            const uint32_t z0 = alloc(2 * h);
+            node(lvl + 1, uo, un, vo, vn, h, z0, 2 * h);
+            if (combs.size() <= lvl) combs.resize(lvl + 1);
+            combs[lvl].push_back({z0, kKaNone, z0, r, rcap});
+            return;
+        }
+        struct Half {
+            uint32_t lo_n, hi_o, hi_n, s_o, s_n;
+        };
+        auto half = [&](uint32_t o, uint32_t len) {
+            Half x;
+            x.lo_n = std::min(len, h);
+            x.hi_o = o + h;
+            x.hi_n = len > h ? len - h : 0u;
+            if (x.hi_n == 0) { // lo + hi = lo: no sum to form
+                x.s_o = o, x.s_n = x.lo_n;
+            } else {
+                x.s_o = alloc(h), x.s_n = h;
+                if (sums.size() <= lvl) sums.resize(lvl + 1);
+                sums[lvl].push_back({o, len, x.s_o});
+            }
+            return x;
+        };
+        const Half U = half(uo, un), V = half(vo, vn);
+        const bool has_z1 = U.hi_n && V.hi_n;
+        const uint32_t z0 = alloc(2 * h), z2 = alloc(2 * h);
+        const uint32_t z1 = has_z1 ? alloc(2 * h) : kKaNone;
+        node(lvl + 1, uo, U.lo_n, vo, V.lo_n, h, z0, 2 * h);
+        if (has_z1) node(lvl + 1, U.hi_o, U.hi_n, V.hi_o, V.hi_n, h, z1, 2 * h);
+        node(lvl + 1, U.s_o, U.s_n, V.s_o, V.s_n, h, z2, 2 * h);
+        if (combs.size() <= lvl) combs.resize(lvl + 1);
+        combs[lvl].push_back({z0, z1, z2, r, rcap});
+    }
+};
+
+} // namespace
+
 // Symbolic run.  Slot offsets are first relative to their region (in / pp / prefix / carries of
 // even columns / carries of odd columns); regions are placed once their maxima are known.
 bool build_plan(MulPlan &P) {
     const uint32_t K = P.K;
-    enum { IN, PP, PRE, CA, CB, NREG };
+    enum { IN, PP, PRE, CA, CB, KA, NREG };
     Region reg[NREG];
     std::vector<uint8_t> slot_reg;
     auto new_slot = [&](int r, int64_t bound) -> uint32_t {
@@ -149,9 +243,59 @@ bool build_plan(MulPlan &P) {
         col.res = new_slot(PRE, -1); // degree-only slot (the output bit)
         P.res_slots.push_back(col.res);
         P.res_bound[i] = pb;
-        // tiles of this column's products, grouped by per-lane width
+        // Karatsuba for the big products (their slots are final now: region offsets are fixed
+        // when the regions are placed, so views are recorded relative and fixed up below)
+        std::vector<bool> is_ka(P.prod.size() - col.prod, false);
+        for (uint32_t k = col.prod; k < P.prod.size() && P.ka_min; ++k) {
+            const MulProdTask &T = P.prod[k];
+            const uint32_t nu = P.slots[T.u].words, nv = P.slots[T.v].words;
+            if (std::min(nu, nv) < P.ka_min) continue;
+            uint32_t lk = 0;
+            while (((uint64_t)P.ka_leaf << lk) < std::max(nu, nv)) ++lk;
+            if (lk == 0) continue;
+            // leaf: the smallest multiple of 32 words with leaf * 2^lk >= max(nu, nv)
+            const uint32_t mx = std::max(nu, nv);
+            const uint32_t leaf = (((mx + (1u << lk) - 1) >> lk) + 31) & ~31u;
+            KaBuild kb{(uint32_t)KA, leaf};
+            auto view = [&](uint32_t slot) {
+                return ((uint32_t)slot_reg[slot] << kRegShift) | P.slots[slot].off;
+            };
+            kb.node(0, view(T.u), nu, view(T.v), nv, leaf << lk, view(T.out), P.slots[T.out].words);
+            reg[KA].max = std::max(reg[KA].max, kb.max);
+            KaProg pg;
+            pg.u = T.u, pg.v = T.v, pg.out = T.out;
+            for (uint32_t l = 0; l < kb.sums.size(); ++l) {
+                if (kb.sums[l].empty()) continue;
+                pg.sums.push_back({(uint32_t)P.ka_sums.size(), (uint32_t)kb.sums[l].size(),
+                                   (leaf << lk) >> (l + 1)});
+                P.ka_sums.insert(P.ka_sums.end(), kb.sums[l].begin(), kb.sums[l].end());
+            }
+            pg.vtask = (uint32_t)P.ka_vtasks.size(), pg.nvtask = (uint32_t)kb.leaves.size();
+            P.ka_vtasks.insert(P.ka_vtasks.end(), kb.leaves.begin(), kb.leaves.end());
+            uint32_t wc = kNW - 1;
+            for (uint32_t q = 0; q < kNW; ++q)
+                if (kMulTileW[q] * 64 >= 2 * leaf) {
+                    wc = q;
+                    break;
+                }
+            pg.tiles[wc] = (uint32_t)P.ka_vtiles.size();
+            for (uint32_t t = 0; t < pg.nvtask; ++t)
+                for (uint32_t b0 = 0; b0 < 2 * leaf; b0 += 64 * kMulTileW[wc])
+                    P.ka_vtiles.push_back({t, b0});
+            pg.ntiles[wc] = (uint32_t)P.ka_vtiles.size() - pg.tiles[wc];
+            for (uint32_t l = (uint32_t)kb.combs.size(); l-- > 0;) {
+                if (kb.combs[l].empty()) continue;
+                pg.combs.push_back({(uint32_t)P.ka_combs.size(), (uint32_t)kb.combs[l].size(),
+                                    (leaf << lk) >> (l + 1)});
+                P.ka_combs.insert(P.ka_combs.end(), kb.combs[l].begin(), kb.combs[l].end());
+            }
+            col.ka.push_back(std::move(pg));
+            is_ka[k - col.prod] = true;
+        }
+        // tiles of this column's schoolbook products, grouped by per-lane width
         std::vector<MulTile> byw[kNW];
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
+            if (is_ka[k - col.prod]) continue;
             const uint32_t nout = P.slots[P.prod[k].out].words;
             const uint32_t need = (nout + 63) / 64;
             uint32_t wc = kNW - 1;
@@ -172,6 +316,8 @@ bool build_plan(MulPlan &P) {
         prev.swap(cur);
     }
     // place the regions and make the offsets absolute
+    for (int r = 0; r < NREG; ++r)
+        if (reg[r].max >= (1ull << kRegShift)) return false; // planning views hold 28-bit offsets
     uint64_t base = 0;
     for (int r = 0; r < NREG; ++r) {
         reg[r].base = base;
@@ -179,6 +325,13 @@ bool build_plan(MulPlan &P) {
     }
     if (base >= (1ull << 32)) return false;
     for (size_t s = 0; s < P.slots.size(); ++s) P.slots[s].off += (uint32_t)reg[slot_reg[s]].base;
+    // Karatsuba views: (region, relative offset) -> arena offset
+    auto fix = [&](uint32_t o) -> uint32_t {
+        return o == kKaNone ? o : (uint32_t)(reg[o >> kRegShift].base + (o & kRelMask));
+    };
+    for (auto &t : P.ka_sums) t.src = fix(t.src), t.dst = fix(t.dst);
+    for (auto &t : P.ka_vtasks) t.u = fix(t.u), t.v = fix(t.v), t.out = fix(t.out);
+    for (auto &t : P.ka_combs) t.z0 = fix(t.z0), t.z1 = fix(t.z1), t.z2 = fix(t.z2), t.r = fix(t.r);
     P.astride = std::max<uint64_t>(base, 4);
     return true;
 }
@@ -192,6 +345,10 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_prod = o, o = align(o + P.prod.size() * sizeof(MulProdTask));
     P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
+    P.off_ka_sums = o, o = align(o + P.ka_sums.size() * sizeof(KaSum));
+    P.off_ka_vtasks = o, o = align(o + P.ka_vtasks.size() * sizeof(MulVTask));
+    P.off_ka_vtiles = o, o = align(o + P.ka_vtiles.size() * sizeof(MulVTile));
+    P.off_ka_combs = o, o = align(o + P.ka_combs.size() * sizeof(KaComb));
     std::vector<uint8_t> h(std::max<size_t>(o, 16), 0);
     auto put = [&](size_t off, const void *src, size_t n) {
         if (n) std::memcpy(h.data() + off, src, n);
@@ -202,6 +359,10 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_prod, P.prod.data(), P.prod.size() * sizeof(MulProdTask));
     put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
+    put(P.off_ka_sums, P.ka_sums.data(), P.ka_sums.size() * sizeof(KaSum));
+    put(P.off_ka_vtasks, P.ka_vtasks.data(), P.ka_vtasks.size() * sizeof(MulVTask));
+    put(P.off_ka_vtiles, P.ka_vtiles.data(), P.ka_vtiles.size() * sizeof(MulVTile));
+    put(P.off_ka_combs, P.ka_combs.data(), P.ka_combs.size() * sizeof(KaComb));
     DeviceGuard g(c->device);
     HM_HIP(c, hipStreamSynchronize(c->stream));
     HM_HIP(c, hipMalloc(&P.d_tab, h.size()));
@@ -215,13 +376,15 @@ constexpr size_t kMaxPlans = 8;
 hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const uint32_t *bb,
                    bool is_signed, MulPlan *&out) {
     for (MulPlan *p : c->mul_plans)
-        if (p->L == L && p->K == K && p->is_signed == is_signed &&
+        if (p->L == L && p->K == K && p->is_signed == is_signed && p->ka_min == c->ka_min &&
+            p->ka_leaf == c->ka_leaf &&
             std::equal(p->ab.begin(), p->ab.end(), ab) && std::equal(p->bb.begin(), p->bb.end(), bb)) {
             out = p;
             return HM_OK;
         }
     auto P = std::make_unique<MulPlan>();
     P->L = L, P->K = K, P->is_signed = is_signed;
+    P->ka_min = c->ka_min, P->ka_leaf = c->ka_leaf;
     P->ab.assign(ab, ab + K), P->bb.assign(bb, bb + K);
     if (!build_plan(*P)) return HM_ERR_UNSUPPORTED;
     if (hm_status st = upload_plan(c, *P); st) {
@@ -285,6 +448,37 @@ void mul_plans_release(hm_ctx *c) {
     }
     c->mul_plans.clear();
 }
+
+namespace {
+
+// the launches of one Karatsuba product: sums by depth, leaf products, recombination bottom-up,
+// and the exact output degree
+hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B) {
+    const uint8_t *T = P.d_tab;
+    for (const auto &lv : pg.sums) {
+        KaSumArgs a{};
+        a.B = B, a.t = (const KaSum *)(T + P.off_ka_sums) + lv[0], a.nt = lv[1], a.h = lv[2];
+        if (launch_ka_sum(a, c->stream)) return hip_fail(c, hipGetLastError());
+    }
+    for (uint32_t q = 0; q < kNW; ++q) {
+        if (!pg.ntiles[q]) continue;
+        MulVProdArgs a{};
+        a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
+        a.tiles = (const MulVTile *)(T + P.off_ka_vtiles) + pg.tiles[q], a.ntiles = pg.ntiles[q];
+        if (launch_mul_vprod(a, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
+    }
+    for (const auto &lv : pg.combs) {
+        KaCombArgs a{};
+        a.B = B, a.t = (const KaComb *)(T + P.off_ka_combs) + lv[0], a.nt = lv[1], a.h = lv[2];
+        if (launch_ka_comb(a, c->stream)) return hip_fail(c, hipGetLastError());
+    }
+    MulDegArgs d{};
+    d.B = B, d.u = pg.u, d.v = pg.v, d.out = pg.out;
+    if (launch_mul_deg(d, c->stream)) return hip_fail(c, hipGetLastError());
+    return HM_OK;
+}
+
+} // namespace
 
 hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t K, bool is_signed,
                       hm_batch *out) {
@@ -350,6 +544,8 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 pr.ntiles = col.ntiles[q];
                 if (launch_mul_prod(pr, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
             }
+            for (const KaProg &pg : col.ka) // one Karatsuba product at a time (shared scratch)
+                if (hm_status st = run_ka(c, *P, pg, B); st) return st;
         }
         MulFinalArgs F{};
         F.B = B, F.res = (const uint32_t *)(T + P->off_res), F.K = K, F.out = oa;

@@ -428,6 +428,13 @@ class Context:
                               "(run more warm-up calls)")
         return EngineGraph(self, g, gen)
 
+    def set_mul_options(self, karatsuba_min_words: int = 1024, karatsuba_leaf_words: int = 256):
+        """hm_ctx_set_mul_options: which carry products of the multiplier run as Karatsuba
+        recursions (shorter operand >= karatsuba_min_words words; 0 = never) and their leaf
+        size.  Results are identical either way (every product is exact)."""
+        _check(lib().hm_ctx_set_mul_options(self._h, karatsuba_min_words, karatsuba_leaf_words),
+               "hm_ctx_set_mul_options")
+
     def generation(self) -> int:
         return int(lib().hm_ctx_generation(self._h))
 

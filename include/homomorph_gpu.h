@@ -148,6 +148,14 @@ hm_status hm_ctx_get_secret_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
 hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, uint32_t *tau,
                                 uint32_t *limbs_per_poly);
 
+/* Multiplier strategy (no effect on results: every product is exact).  A carry product of the
+ * carry-save circuit whose shorter operand has at least karatsuba_min_words 32-bit words runs as
+ * a Karatsuba recursion down to leaves of at most karatsuba_leaf_words
+ * words (rounded to a multiple of 32); smaller products run as schoolbook tiles.
+ * karatsuba_min_words = 0 disables it.  Defaults: 1024 and 256. */
+hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
+                                 uint32_t karatsuba_leaf_words);
+
 /* Context::validate_operation (src/context.rs:310-323): HM_OK or HM_ERR_INVALID_PARAMETERS with
  * the OperationError payload written to *required_min_d_over_delta (may be NULL). */
 hm_status hm_validate_operation(const hm_ctx *ctx, hm_op op, uint16_t *required_min_d_over_delta);

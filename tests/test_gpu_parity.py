@@ -341,3 +341,60 @@ def test_mul_low_parity(H, oracle, k, n):
         want = ((a.astype(np.uint64) * b) & ((1 << k) - 1)).astype(np.uint64)
         got = dec_bytes.astype(np.uint64) @ (256 ** np.arange(k // 8, dtype=np.uint64))
         assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("ka_min,leaf", [(32, 32), (64, 96), (128, 256)])
+def test_mul_karatsuba_parity(H, oracle, ka_min, leaf):
+    """The Karatsuba carry products (hm_ctx_set_mul_options) forced down
+    to small sizes: u8 multiply and the u32 low-12 prefix, bit-exact vs the oracle's bit-serial
+    products, and equal to the schoolbook-only engine (karatsuba_min_words = 0)."""
+    from helpers import low_bits
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 91)
+    ctx.set_mul_options(ka_min, leaf)
+    sk, pk, _ = keys(*params, 91)
+    bound = fresh_bound(128, 128, 32)
+    # u8: products up to ~450 words
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, np.uint8, 4, 92)
+    cp = ctx.apply2(H.HomomorphicMultiplication, ca, cb)
+    ctx.synchronize()
+    b8 = fresh_bound(128, 128, 8)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, b8)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, b8)
+    rl, rd = oracle.mul_batch(la, da, b8, lb, db, b8, 8, 4, cp.bound)
+    gl, gd = cp.to_host()
+    assert_batches_equal(gl, gd, rl, rd, cp.bound, 4, f"u8 karatsuba {ka_min}/{leaf}")
+    # u32, low 12 result bits: products up to ~2500 words, several recursion levels
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, np.uint32, 2, 93)
+    cp = ctx.mul_low(ca, cb, 12)
+    ctx.synchronize()
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    lak, dak, bk = low_bits(la, da, bound, 2, 12)
+    lbk, dbk, _ = low_bits(lb, db, bound, 2, 12)
+    rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, 12, 2, cp.bound)
+    gl, gd = cp.to_host()
+    assert_batches_equal(gl, gd, rl, rd, cp.bound, 2, f"u32 low-12 karatsuba {ka_min}/{leaf}")
+    ctx.set_mul_options(0, 256)  # schoolbook only: the same bits
+    cs = ctx.mul_low(ca, cb, 12)
+    ctx.synchronize()
+    sl, sd = cs.to_host()
+    assert_batches_equal(sl, sd, gl, gd, cp.bound, 2, "schoolbook vs karatsuba")
+
+
+def test_mul_karatsuba_low16_matches_schoolbook(H):
+    """At the bench's K = 16 (products up to ~28k words, 6-7 recursion levels) the default
+    Karatsuba path and the schoolbook-only path give identical ciphertexts (the K = 16 golden
+    fixture pins the default path to the oracle, tests/test_golden.py)."""
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 95)
+    x = plain(3, np.uint32, 96)
+    ca, cb = ctx.encrypt(x), ctx.encrypt(x[::-1].copy())
+    ka = ctx.mul_low(ca, cb, 16)
+    ctx.synchronize()
+    ctx.set_mul_options(0, 256)
+    sb = ctx.mul_low(ca, cb, 16)
+    ctx.synchronize()
+    kl, kd = ka.to_host()
+    sl, sd = sb.to_host()
+    assert_batches_equal(kl, kd, sl, sd, ka.bound, 3, "K=16 karatsuba vs schoolbook")
