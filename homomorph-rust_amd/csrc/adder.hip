@@ -1,0 +1,347 @@
+// adder.hip — gfx950 kernels of the ripple-carry adder (src/impls/numbers/common.rs:37-56):
+//   add_prep_kernel          carry-independent part: ab_i, P_i, x_i for every bit, lanes over
+//                            (bit, word), several waves per value
+//   add_chain_staged_kernel / add_chain_kernel
+//                            the carry chain carry' = ab_i ^ P_i * carry, one wavefront per
+//                            value, carry kept in LDS
+#include <hip/hip_runtime.h>
+
+#include "dev_common.h"
+
+namespace hm {
+
+// ---------------------------------------------------------------------------------------------
+// Ripple-carry adder (common.rs:37-56).  Per bit i (common.rs:43-53):
+//   x = a_i ^ b_i;  s_i = x ^ carry;
+//   carry' = (x & carry) ^ (a_i & b_i) & ((x & carry) ^ 1)
+//          = ab_i ^ P_i * carry,   ab_i = a_i b_i,   P_i = x (1 ^ ab_i)   (GF(2)[X] ring identity)
+// ab_i and P_i do not depend on the carry: add_prep_kernel computes all of them in parallel
+// (several waves per value, lanes over (bit, output word), branch-free per-lane products), then
+// add_chain_kernel runs the sequential chain with ONE product per bit, P_i * carry, where P_i is
+// wave-uniform (scalar loads, scalar branches over its bits, Horner over bit positions) and the
+// carry stays in LDS for the whole chain.
+
+__device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
+    uint32_t o = 0;
+    for (uint32_t j = 0; j < i; ++j) o += cap_of(B.b[j]);
+    return o;
+}
+
+// Stage bits [i0, i0+nb) of one value's input (u64 limbs, exact degrees) into LDS words: bit
+// i0+t at dst + t*cnt, its word count at nw[t] (0 = null).  Lanes stride over the range's
+// contiguous limbs (all its bits at once, coalesced); every limb is validated against its bit's
+// degree word as in load_bit.  src/deg point at the value's first limb / degree word.
+__device__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
+                           const Bounds &B, uint32_t i0, uint32_t nb, uint32_t *dst, uint32_t cnt,
+                           uint32_t *nw, int *status) {
+    const int lane = lane_id();
+    src += limb_off(B, i0);
+    deg += i0;
+    uint32_t total = 0;
+    for (uint32_t t = 0; t < nb; ++t) total += cap_of(B.b[i0 + t]);
+    uint32_t t = 0, lo = 0, hi = nb ? cap_of(B.b[i0]) : 0;
+    bool bad = false;
+    for (uint32_t g = lane; g < total; g += kWave) {
+        while (g >= hi) ++t, lo = hi, hi += cap_of(B.b[i0 + t]);
+        const uint32_t d = deg[t], k = g - lo;
+        uint64_t v = src[g];
+        if (d > B.b[i0 + t]) {
+            bad = true;
+            continue;
+        }
+        const uint32_t nl = d / 64 + 1;
+        if (k >= nl) {
+            bad |= v != 0; // limbs above the degree must be zero (layout invariant)
+            continue;
+        }
+        if (k == nl - 1) {
+            const uint32_t tb = d % 64;
+            const uint64_t keep = (~0ull) >> (63 - tb);
+            bad |= (v & ~keep) != 0;
+            v &= keep;
+            if (d > 0 && !((v >> tb) & 1ull)) bad = true;
+        }
+        dst[t * cnt + 2 * k] = (uint32_t)v;
+        dst[t * cnt + 2 * k + 1] = (uint32_t)(v >> 32);
+    }
+    if (__any(bad) && lane == 0) flag(status, HM_ERR_BAD_INPUT);
+    wsync();
+    for (uint32_t k = lane; k < nb; k += kWave) {
+        const uint32_t d = deg[k];
+        uint32_t n = d / 32 + 1;
+        if (d > B.b[i0 + k] || (d == 0 && !(dst[k * cnt] & 1u))) n = 0;
+        nw[k] = n;
+    }
+}
+
+__global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t wave = rfl(threadIdx.x >> 6);
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint64_t e = gw / A.wpv;
+    const uint32_t part = (uint32_t)(gw % A.wpv);
+    if (e >= A.n) return;
+    const int lane = lane_id();
+    const uint32_t L = A.nbits;
+    const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits [i0, i0 + nmine)
+    const uint32_t i0 = min(L, part * bpw), nmine = min(L, i0 + bpw) - i0;
+    // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][P: bpw cntP][na nb dAB dP]
+    uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
+    uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
+    uint32_t *ABl = Xl + bpw * A.cntX, *Pl = ABl + bpw * A.cntAB;
+    uint32_t *nAl = Pl + bpw * A.cntP, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
+    uint32_t *ws = A.ws + e * A.ws_stride;
+    uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
+    const uint64_t *pa = A.a.limbs + e * A.a.stride, *pb = A.b.limbs + e * A.b.stride;
+    const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
+
+    // stage + validate this wave's bits (every bit is validated, the last one too)
+    stage_bits(pa, da, A.ab, i0, nmine, Al, A.cntA, nAl, A.status);
+    stage_bits(pb, db, A.bb, i0, nmine, Bl, A.cntB, nBl, A.status);
+    for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
+    wsync();
+    // products only for bits < L-1 (the last bit has no outgoing carry)
+    const uint32_t nprod = min(nmine, (L - 1) - min(i0, L - 1));
+
+    // x_i = a_i ^ b_i for every bit: LDS for the P products, workspace for the chain's sum bits
+    for (uint32_t f = lane; f < nmine * A.cntX; f += kWave) {
+        const uint32_t t = f / A.cntX, m = f % A.cntX, i = i0 + t;
+        const int na = (int)nAl[t], nb = (int)nBl[t];
+        const uint32_t x = ((int)m < na ? Al[t * A.cntA + m] : 0u) ^
+                           ((int)m < nb ? Bl[t * A.cntB + m] : 0u);
+        Xl[t * A.cntX + m] = x;
+        Xg[(size_t)i * A.cntX + m] = x;
+    }
+
+    // Products by rows: lanes over (slot t, multiplier word q) -- every lane of a slot runs the
+    // same number of steps (the multiplicand's length), rows meet in LDS through ds_xor.
+    const uint32_t cq = A.cntX; // multiplier words: a_i (phase 1) and x_i (phase 2) fit in cntX
+    auto for_rows = [&](auto &&row) {
+        const uint32_t dt = kWave / cq, dq = kWave % cq;
+        uint32_t t = (uint32_t)lane / cq, q = (uint32_t)lane % cq;
+        for (uint32_t f0 = 0; f0 < nprod * cq; f0 += kWave) {
+            if (t < nprod) row(t, q);
+            t += dt, q += dq;
+            if (q >= cq) q -= cq, ++t;
+        }
+    };
+    // phase 1: ab_i = a_i * b_i
+    for (uint32_t k = lane; k < nprod * A.cntAB; k += kWave) ABl[k] = 0u;
+    for (uint32_t k = lane; k < nprod * A.cntP; k += kWave) Pl[k] = 0u;
+    wsync();
+    for_rows([&](uint32_t t, uint32_t q) {
+        if ((int)q < (int)nAl[t])
+            clmul_row_xor(Al[t * A.cntA + q], Bl + t * A.cntB, (int)nBl[t], ABl + t * A.cntAB + q);
+    });
+    wsync();
+    for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
+        const uint32_t t = f / A.cntAB, m = f % A.cntAB;
+        const uint32_t w = ABl[f];
+        ABg[(size_t)(i0 + t) * A.cntAB + m] = w;
+        if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
+    }
+    wsync();
+    // phase 2: P_i = x_i ^ x_i * ab_i
+    for_rows([&](uint32_t t, uint32_t q) {
+        const int nx = max((int)nAl[t], (int)nBl[t]);
+        if ((int)q < nx)
+            clmul_row_xor(Xl[t * A.cntX + q], ABl + t * A.cntAB, bitwords((int)dAB[t]),
+                          Pl + t * A.cntP + q);
+    });
+    wsync();
+    for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) {
+        const uint32_t t = f / A.cntP, m = f % A.cntP;
+        const uint32_t w = Pl[f] ^ (m < A.cntX ? Xl[t * A.cntX + m] : 0u);
+        Pg[(size_t)(i0 + t) * A.cntP + m] = w;
+        if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
+    }
+    wsync();
+    for (uint32_t t = lane; t < nprod; t += kWave) {
+        const uint32_t i = i0 + t;
+        degABg[i] = dAB[t];
+        degPg[i] = dP[t];
+    }
+}
+
+// s_i = a_i ^ b_i ^ carry, read straight from the input limbs (masked at the degrees, which the
+// prep kernel validated) and the LDS carry words; writes the output bit and its exact degree.
+__device__ int store_sum_bit(const uint64_t *pa, uint32_t dga, const uint64_t *pb, uint32_t dgb,
+                             const uint32_t *C, int nc, uint64_t *__restrict__ dst, uint32_t bound,
+                             uint32_t *deg_out, int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int nla = (int)(dga >> 6) + 1, nlb = (int)(dgb >> 6) + 1;
+    const uint64_t ma = (~0ull) >> (63 - (dga & 63)), mb = (~0ull) >> (63 - (dgb & 63));
+    const int total = max(max(cap, max(nla, nlb)), (nc + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        uint64_t v = 0;
+        if (g < nla) v ^= g == nla - 1 ? (pa[g] & ma) : pa[g];
+        if (g < nlb) v ^= g == nlb - 1 ? (pb[g] & mb) : pb[g];
+        const int w = 2 * g;
+        const uint32_t lo = w < nc ? C[w] : 0u, hi = w + 1 < nc ? C[w + 1] : 0u;
+        v ^= (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+template <int WMAX, bool PAD>
+__global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    const uint32_t L = A.nbits;
+    uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
+    uint32_t *C = Ls + kHalo, *Cn = C + A.cw + kHalo;
+    uint32_t *Pl = Cn + A.cw; // P_i slots, copied once from the workspace (uniform reads per step)
+    const uint32_t *ws = A.ws + e * A.ws_stride;
+    const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L;
+    const uint64_t *pa = A.a.limbs + e * A.a.stride, *pb = A.b.limbs + e * A.b.stride;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
+    uint32_t *dout = A.out.degree + e * L;
+
+    // zero both carry buffers with their halos: window reads need no bounds checks (PAD)
+    const uint32_t ncarry = 2 * (A.cw + kHalo);
+    for (uint32_t k = lane; k < ncarry; k += kWave) Ls[k] = 0u;
+    for (uint32_t k = lane; k < (L - 1) * A.cntP; k += kWave) Pl[k] = Pg[k];
+    wsync();
+    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    uint32_t offa = 0, offb = 0, offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        store_sum_bit(pa + offa, rfl(da[i]), pb + offb, rfl(db[i]), C, nc, po + offo, A.ob.b[i],
+                      dout + i, A.status);
+        if (i + 1 < L) {
+            const int np = bitwords((int)degPg[i]), nab = bitwords((int)degABg[i]);
+            int nout;
+            nc = words_of(wave_mul<kQBig, WMAX, PAD>(Pl + (size_t)i * A.cntP, np, C, nc,
+                                                     ABg + (size_t)i * A.cntAB, nab, Cn, &nout));
+            wsync();
+            uint32_t *t = C;
+            C = Cn;
+            Cn = t;
+        }
+        offa += cap_of(A.ab.b[i]);
+        offb += cap_of(A.bb.b[i]);
+        offo += cap_of(A.ob.b[i]);
+    }
+}
+
+// Staged chain (PAD plans whose slots fit in LDS).  Everything the loop reads per bit -- x_i,
+// ab_i, P_i and the product degrees -- is copied from the workspace into LDS once, and the carry
+// is updated in place (PAD products read their whole window before writing their tile), so the
+// only global traffic inside the loop is the output stores: no load ever waits behind them.
+__device__ int store_sum_x(const uint32_t *X, int nx, const uint32_t *C, int nc,
+                           uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
+                           int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int total = max(cap, (max(nx, nc) + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        const uint32_t lo = (w < nx ? X[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        const uint32_t hi = (w + 1 < nx ? X[w + 1] : 0u) ^ (w + 1 < nc ? C[w + 1] : 0u);
+        const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
+template <int WMAX>
+__global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    const uint32_t L = A.nbits;
+    // LDS: [halo][C: cw][P: (L-1) cntP][AB: (L-1) cntAB][X: L cntX][degP: L][degAB: L]
+    uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
+    uint32_t *C = Ls + kHalo;
+    uint32_t *Pl = C + A.cw, *ABl = Pl + (size_t)(L - 1) * A.cntP;
+    uint32_t *Xl = ABl + (size_t)(L - 1) * A.cntAB, *dPl = Xl + (size_t)L * A.cntX, *dABl = dPl + L;
+    const uint32_t *ws = A.ws + e * A.ws_stride;
+    const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    uint32_t *dout = A.out.degree + e * L;
+
+    for (uint32_t k = lane; k < kHalo + A.cw; k += kWave) Ls[k] = 0u;
+    for (uint32_t k = lane; k < (L - 1) * A.cntP; k += kWave) Pl[k] = Pg[k];
+    for (uint32_t k = lane; k < (L - 1) * A.cntAB; k += kWave) ABl[k] = ABg[k];
+    for (uint32_t k = lane; k < L * A.cntX; k += kWave) Xl[k] = Xg[k];
+    for (uint32_t k = lane; k < L; k += kWave) dPl[k] = degPg[k], dABl[k] = degABg[k];
+    wsync();
+    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    uint32_t offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        store_sum_x(Xl + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
+                    A.status);
+        if (i + 1 < L) {
+            const int np = bitwords((int)rfl(dPl[i])), nab = bitwords((int)rfl(dABl[i]));
+            int nout;
+            wsync(); // the sum bit's reads of C precede the in-place product's writes
+            nc = words_of(wave_mul<kQBig, WMAX, true>(Pl + (size_t)i * A.cntP, np, C, nc,
+                                                      ABl + (size_t)i * A.cntAB, nab, C, &nout));
+            wsync();
+        }
+        offo += cap_of(A.ob.b[i]);
+    }
+}
+
+int launch_add(const AddArgs &a, void *stream) {
+    if (a.n == 0) return 0;
+    // prep: wpv waves per value, 4 waves per block
+    {
+        const uint64_t waves = a.n * a.wpv;
+        const uint64_t blocks = (waves + 3) / 4;
+        hipLaunchKernelGGL(add_prep_kernel, dim3((unsigned)blocks), dim3(256),
+                           (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    const int wpb = kAddWavesPerBlock;
+    const uint64_t blocks = (a.n + wpb - 1) / wpb;
+    const size_t lds = (size_t)a.chain_lds * 4 * wpb;
+    // the widest per-lane tile the carry chain needs (carry + P words over 64 lanes)
+    const uint32_t need = (a.max_prod_words + 63) / 64;
+    const bool pad = a.pad != 0;
+#define HM_LAUNCH_ADD(WM)                                                                         \
+    do {                                                                                          \
+        if (a.staged)                                                                             \
+            hipLaunchKernelGGL((add_chain_staged_kernel<WM>), dim3((unsigned)blocks),             \
+                               dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
+        else if (pad)                                                                             \
+            hipLaunchKernelGGL((add_chain_kernel<WM, true>), dim3((unsigned)blocks),              \
+                               dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
+        else                                                                                      \
+            hipLaunchKernelGGL((add_chain_kernel<WM, false>), dim3((unsigned)blocks),             \
+                               dim3(64 * wpb), lds, (hipStream_t)stream, a);                      \
+    } while (0)
+    if (need <= 4) HM_LAUNCH_ADD(4);
+    else if (need <= 8) HM_LAUNCH_ADD(8);
+    else if (need <= 12) HM_LAUNCH_ADD(12);
+    else if (need <= 16) HM_LAUNCH_ADD(16);
+    else HM_LAUNCH_ADD(24);
+#undef HM_LAUNCH_ADD
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace hm

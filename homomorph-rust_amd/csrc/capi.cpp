@@ -608,10 +608,15 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     auto even = [](uint32_t v) { return (v + 1) & ~1u; };
     AddArgs A{};
     A.cntA = cntA, A.cntB = cntB, A.cntAB = cntAB, A.cntP = cntP, A.cntX = cntX;
-    // prep: enough waves per value to keep the chip busy (bits are dealt round-robin)
+    // prep: enough waves per value to keep the chip busy, and at least enough that one wave's
+    // product rows (bits x multiplier words) fit its 64 lanes in one pass (bits are dealt in
+    // contiguous ranges)
     {
         const uint64_t want = (16384 + a->n - 1) / a->n;
-        A.wpv = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 8, (uint64_t)L}));
+        const uint64_t rows_fit = (L + std::max<uint32_t>(1, 64 / cntX) - 1) /
+                                  std::max<uint32_t>(1, 64 / cntX);
+        A.wpv = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>({std::max(want, rows_fit), 8, (uint64_t)L}));
         const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
         A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 4 * bpw);
         if ((size_t)A.prep_lds * 4 * 4 > 160 * 1024) return HM_ERR_UNSUPPORTED;

@@ -237,6 +237,7 @@ int launch_poly_mul(const PolyArgs &a, void *stream);
 int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
-constexpr size_t kEncTableBytes = 64 * 1024; // largest encryption nibble table staged in LDS
+constexpr size_t kEncTableBytes = 96 * 1024; // largest encryption nibble table staged in LDS
+                                              // (tau = 256 at d + dp = 512: 80 KB)
 
 } // namespace hm

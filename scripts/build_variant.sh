@@ -5,10 +5,10 @@ cd "$(dirname "$0")/../homomorph-rust_amd"
 name=$1; shift
 tmp=$(mktemp -d)
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 $*"
-/opt/rocm/bin/hipcc $F -c csrc/kernels.hip -o $tmp/k.o &
-/opt/rocm/bin/hipcc $F -x hip -c csrc/capi.cpp -o $tmp/c.o &
-wait %1 && wait %2
+for f in kernels adder cipher mul_engine; do /opt/rocm/bin/hipcc $F -c csrc/$f.hip -o $tmp/$f.o & done
+for f in capi mul_host wire; do /opt/rocm/bin/hipcc $F -x hip -c csrc/$f.cpp -o $tmp/$f.o & done
+wait
 mkdir -p lib/var
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/var/lib$name.so $tmp/k.o $tmp/c.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/var/lib$name.so $tmp/*.o
 rm -rf $tmp
 echo lib/var/lib$name.so
