@@ -31,7 +31,7 @@ __device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
 // i0+t at dst + t*cnt, its word count at nw[t] (0 = null).  Lanes stride over the range's
 // contiguous limbs (all its bits at once, coalesced); every limb is validated against its bit's
 // degree word as in load_bit.  src/deg point at the value's first limb / degree word.
-__device__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
+__device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
                            const Bounds &B, uint32_t i0, uint32_t nb, uint32_t *dst, uint32_t cnt,
                            uint32_t *nw, int *status) {
     const int lane = lane_id();
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
 
 // s_i = a_i ^ b_i ^ carry, read straight from the input limbs (masked at the degrees, which the
 // prep kernel validated) and the LDS carry words; writes the output bit and its exact degree.
-__device__ int store_sum_bit(const uint64_t *pa, uint32_t dga, const uint64_t *pb, uint32_t dgb,
+__device__ __forceinline__ int store_sum_bit(const uint64_t *pa, uint32_t dga, const uint64_t *pb, uint32_t dgb,
                              const uint32_t *C, int nc, uint64_t *__restrict__ dst, uint32_t bound,
                              uint32_t *deg_out, int *status) {
     const int lane = lane_id();
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
 // ab_i, P_i and the product degrees -- is copied from the workspace into LDS once, and the carry
 // is updated in place (PAD products read their whole window before writing their tile), so the
 // only global traffic inside the loop is the output stores: no load ever waits behind them.
-__device__ int store_sum_x(const uint32_t *X, int nx, const uint32_t *C, int nc,
+__device__ __forceinline__ int store_sum_x(const uint32_t *X, int nx, const uint32_t *C, int nc,
                            uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
                            int *status) {
     const int lane = lane_id();

@@ -33,7 +33,7 @@ __device__ __forceinline__ uint32_t cap_of(uint32_t bound) { return bound / 64 +
 // Load one ciphertext bit (u64 limbs, exact degree `deg`) into 32-bit words at dst.
 // The degree word is validated against the limbs (top bit set, nothing above it).
 // Returns the word count (0 for the null polynomial).
-__device__ inline int load_bit(const uint64_t *__restrict__ src, uint32_t deg, uint32_t bound,
+__device__ __forceinline__ int load_bit(const uint64_t *__restrict__ src, uint32_t deg, uint32_t bound,
                         uint32_t *__restrict__ dst, int *status) {
     const int lane = lane_id();
     if (deg > bound) {
@@ -68,7 +68,7 @@ __device__ inline int load_bit(const uint64_t *__restrict__ src, uint32_t deg, u
 }
 
 // dst (cap limbs) = X ^ C; writes the exact degree; returns it (-1 = null).
-__device__ inline int store_xor_bit(const uint32_t *X, int nx, const uint32_t *C, int nc,
+__device__ __forceinline__ int store_xor_bit(const uint32_t *X, int nx, const uint32_t *C, int nc,
                              uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
                              int *status) {
     const int lane = lane_id();
@@ -95,7 +95,7 @@ __device__ inline int store_xor_bit(const uint32_t *X, int nx, const uint32_t *C
 __device__ __forceinline__ int words_of(int deg) { return deg >= 0 ? nwords(deg) : 0; }
 
 // dst (cap limbs) = A ^ B ^ C (output bit of the adder); writes the exact degree.
-__device__ inline int store_xor3_bit(const uint32_t *Aw, int na, const uint32_t *Bw, int nb,
+__device__ __forceinline__ int store_xor3_bit(const uint32_t *Aw, int na, const uint32_t *Bw, int nb,
                               const uint32_t *C, int nc, uint64_t *__restrict__ dst,
                               uint32_t bound, uint32_t *deg_out, int *status) {
     const int lane = lane_id();

@@ -62,13 +62,19 @@ __device__ __forceinline__ void xor3_in(uint32_t &t, uint32_t a, uint32_t b) {
     asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(t) : "v"(a), "v"(b));
 }
 
+// Max over the wave, all in VALU (DPP), no LDS round trips (a __shfl_xor butterfly is six
+// ds_bpermute + s_waitcnt pairs): row_shr 1/2/4/8 leave each row's max in its lane 15,
+// row_bcast:15 / :31 fold the rows into lane 63.  Lanes without a DPP source take INT_MIN.
 __device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        int w = __shfl_xor(v, o, 64);
-        v = v > w ? v : w;
-    }
-    return (int)rfl((uint32_t)v); // uniform: keeps every size derived from it in SGPRs
+    constexpr int kMin = -2147483647 - 1;
+    auto mx = [](int a, int b) { return a > b ? a : b; };
+    v = mx(v, __builtin_amdgcn_update_dpp(kMin, v, 0x111, 0xf, 0xf, false)); // row_shr:1
+    v = mx(v, __builtin_amdgcn_update_dpp(kMin, v, 0x112, 0xf, 0xf, false)); // row_shr:2
+    v = mx(v, __builtin_amdgcn_update_dpp(kMin, v, 0x114, 0xf, 0xf, false)); // row_shr:4
+    v = mx(v, __builtin_amdgcn_update_dpp(kMin, v, 0x118, 0xf, 0xf, false)); // row_shr:8
+    v = mx(v, __builtin_amdgcn_update_dpp(kMin, v, 0x142, 0xa, 0xf, false)); // row_bcast:15
+    v = mx(v, __builtin_amdgcn_update_dpp(kMin, v, 0x143, 0xc, 0xf, false)); // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63); // uniform: sizes derived from it stay in SGPRs
 }
 
 __device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v) {

@@ -73,7 +73,7 @@ __device__ __forceinline__ int poly_words(const uint64_t *limbs, uint32_t deg) {
     return nwords((int)deg);
 }
 
-__device__ void zero_tail_and_degree(uint64_t *out, uint32_t ocap, int deg, uint32_t *odeg,
+__device__ __forceinline__ void zero_tail_and_degree(uint64_t *out, uint32_t ocap, int deg, uint32_t *odeg,
                                      int written_words) {
     uint32_t *w = (uint32_t *)out;
     for (int k = written_words + lane_id(); k < (int)(2 * ocap); k += kWave) w[k] = 0u;

@@ -23,7 +23,7 @@ __device__ __forceinline__ uint32_t *slot_ptr(const MulBase &B, uint32_t s, uint
 
 // one ciphertext bit (u64 limbs + exact degree) -> arena slot (u32 words, zero-filled to the
 // slot's capacity), validated as load_bit does; writes deg1.
-__device__ void stage_one(const MulBase &B, const uint64_t *src, uint32_t deg, uint32_t bound,
+__device__ __forceinline__ void stage_one(const MulBase &B, const uint64_t *src, uint32_t deg, uint32_t bound,
                           uint32_t slot, uint64_t e) {
     const int lane = lane_id();
     uint32_t *dst = slot_ptr(B, slot, e);
