@@ -3,7 +3,8 @@
 //                            (bit, word), several waves per value
 //   add_chain_staged_kernel / add_chain_kernel
 //                            the carry chain carry' = ab_i ^ P_i * carry, one wavefront per
-//                            value, carry kept in LDS
+//                            value, carry kept in LDS, products by scalar-decided VALU XORs
+//                            (the matrix-core chain is adder_mfma.hip)
 #include <hip/hip_runtime.h>
 
 #include "dev_common.h"
@@ -242,29 +243,6 @@ __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
 // ab_i, P_i and the product degrees -- is copied from the workspace into LDS once, and the carry
 // is updated in place (PAD products read their whole window before writing their tile), so the
 // only global traffic inside the loop is the output stores: no load ever waits behind them.
-__device__ __forceinline__ int store_sum_x(const uint32_t *X, int nx, const uint32_t *C, int nc,
-                           uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
-                           int *status) {
-    const int lane = lane_id();
-    const int cap = (int)cap_of(bound);
-    const int total = max(cap, (max(nx, nc) + 1) / 2);
-    int ldeg = -1;
-    for (int g = lane; g < total; g += kWave) {
-        const int w = 2 * g;
-        const uint32_t lo = (w < nx ? X[w] : 0u) ^ (w < nc ? C[w] : 0u);
-        const uint32_t hi = (w + 1 < nx ? X[w + 1] : 0u) ^ (w + 1 < nc ? C[w + 1] : 0u);
-        const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
-        if (g < cap) dst[g] = v;
-        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
-    }
-    const int deg = wave_max_i32(ldeg);
-    if (lane == 0) {
-        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
-        *deg_out = (uint32_t)max(deg, 0);
-    }
-    return deg;
-}
-
 template <int WMAX>
 __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
@@ -317,6 +295,7 @@ int launch_add(const AddArgs &a, void *stream) {
                            (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
         if (hipGetLastError() != hipSuccess) return -1;
     }
+    if (a.mfma) return launch_add_chain_mfma(a, stream);
     const int wpb = kAddWavesPerBlock;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     const size_t lds = (size_t)a.chain_lds * 4 * wpb;

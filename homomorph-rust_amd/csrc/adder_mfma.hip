@@ -1,0 +1,202 @@
+// adder_mfma.hip — the ripple-carry adder's carry chain on the matrix cores (gfx950 fp4 MFMA).
+//
+// The chain (src/impls/numbers/common.rs:37-56) is  carry_{i+1} = ab_i ^ P_i * carry_i  with one
+// carry-less product per bit (adder.hip derives the identity; add_prep_kernel computes ab_i, P_i
+// and x_i).  A GF(2)[X] product is a {0,1} convolution reduced mod 2:
+//     bit k of P*C = ( sum_j P[j] C[k-j] ) mod 2,
+// and v_mfma_scale_f32_32x32x64_f8f6f4 with fp4 (e2m1) operands multiplies {0,1} matrices exactly
+// (products 0/1, f32 accumulation exact below 2^24).  So the product runs as a Toeplitz GEMM:
+//
+//   output tile T = 32 carry words W = 32T + n (MFMA column n) x 32 bit positions m (MFMA row m).
+//   K runs over the carry window of W: words w = W - D + 2c + h (chunk c, lane half h) and their
+//   bits e, so that
+//       out[32W + m] = sum_{c,h,e} A_c[m][(h,e)] * B_c[(h,e)][n]
+//       A_c[m][(h,e)] = P[32(D - 2c - h) + m - e]      (independent of the tile: built once per bit)
+//       B_c[(h,e)][n] = C[32(32T + n - D + 2c + h) + e]
+//   with D = np (np = words of P_i: output word W takes carry words W-np .. W, since word q of P
+//   times word w of the carry reaches output words q+w and q+w+1) and NC = floor(np/2) + 1
+//   chunks of K = 64.  At d+d' = 256 (P_i < 2^769, 25 words) that is 13 MFMAs per 32 output
+//   words, 8 % above the dense bit-pair count.
+//
+// tools/fp4_mfma_probe.hip pins what this relies on: lane l holds A row l%32 and B column l%32,
+// element e of lane half h of A meets element e of lane half h of B, and fp4 reads only the low 4
+// operand VGPRs.  Element e of a fragment is nibble e%8 of VGPR e/8.
+//
+// Per value (one wave), in LDS:
+//   C     the carry as bits (u32 words), zero halo below, updated in place tile by tile from the
+//         top (tile T's output words are no longer read by tiles < T);
+//   ring  nibble images of the carry words the next tiles read (fp4 1.0 per set bit, 16 B per
+//         word, 128 slots mapped twice): a B fragment is one ds_read_b128;
+//   Pst   P_i above kPstLow zero words (the A windows of the chunks past P reach P word -26).
+// A 1 KB table per block maps a byte to its 8 nibbles.
+//
+// Parity: every accumulator starts at 2^23, so after the MFMAs it holds 2^23 + count exactly and
+// bit 0 of its f32 encoding is the coefficient.  One v_alignbit per accumulator gathers them.
+#include <hip/hip_runtime.h>
+
+#include "dev_common.h"
+
+namespace hm {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+constexpr int kPstLow = 28; // zero words below P_i in Pst (64 words: P_i within 25, zeros above)
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
+    // cbsz = blgp = 4: both operands fp4 e2m1; E8M0 scales 127 = 1.0
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
+}
+
+// acc += A * B over the kMfmaChunks chunks of one tile; rb = the tile's window slot (chunk c's B
+// fragment at rb[2c]).  The reads run kPrefetch chunks ahead of the MFMAs.  Left alone, the
+// compiler hoists all 13 reads (13 x 4 VGPRs beside A's 52: spills) and sinks the MFMAs below
+// them; an empty asm after each MFMA that names acc (so the MFMA stays above it: no instruction,
+// no wait) and clobbers memory (so later reads stay below it) pins the interleaving.
+constexpr int kPrefetch = 3;
+__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const uint4 *rb, v16f acc) {
+    uint4 bq[kMfmaChunks];
+#pragma unroll
+    for (int c = 0; c < kPrefetch; ++c) bq[c] = rb[2 * c];
+#pragma unroll
+    for (int c = 0; c < kMfmaChunks; ++c) {
+        if (c + kPrefetch < kMfmaChunks) bq[c + kPrefetch] = rb[2 * (c + kPrefetch)];
+        const v8i Bf = {(int)bq[c].x, (int)bq[c].y, (int)bq[c].z, (int)bq[c].w, 0, 0, 0, 0};
+        acc = mfma_fp4(Af[c], Bf, acc);
+        asm volatile("" : "+v"(acc)::"memory");
+    }
+    return acc;
+}
+
+// Nibble images of carry words [base, base + count) into the ring (count <= 64).  Lane l writes
+// bytes 2h, 2h+1 of word base + k (k = l%32 + 32*pass, h = l/32) as two table lookups.  Every
+// slot is written twice, at s and s + kMfmaRingSlots, so a tile's window [slot, slot + 2*NC) is
+// contiguous wherever it starts: its B reads share one address and differ by immediates.
+__device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, const uint32_t *tab,
+                                          int base, int count) {
+    const int lane = lane_id();
+    const int h = lane >> 5;
+    for (int k = lane & 31; k < count; k += 32) {
+        const int w = base + k;
+        const uint32_t v = C[w] >> (16 * h);
+        uint2 nb;
+        nb.x = tab[v & 0xFFu];
+        nb.y = tab[(v >> 8) & 0xFFu];
+        uint32_t *slot = &ring[(w & (kMfmaRingSlots - 1)) * 4 + 2 * h];
+        *(uint2 *)slot = nb;
+        *(uint2 *)(slot + 4 * kMfmaRingSlots) = nb;
+    }
+}
+
+__global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *tab = lds; // byte -> 8 nibbles, fp4 1.0 (0b0010) per set bit
+    for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v |= ((k >> t) & 1u) << (4 * t + 1);
+        tab[k] = v;
+    }
+    __syncthreads();
+    const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= A.n) return; // whole wave exits together
+    const int lane = lane_id();
+    const int col = lane & 31, h = lane >> 5;
+    const uint32_t L = A.nbits;
+    // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][Pst: 64]
+    uint32_t *Ls = lds + 256 + (size_t)wave * A.chain_lds;
+    uint32_t *C = Ls + kMfmaHalo;
+    uint32_t *ring = C + A.mf_cw;
+    uint32_t *Pst = ring + 8 * kMfmaRingSlots;
+    const uint32_t *ws = A.ws + e * A.ws_stride;
+    const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
+    const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
+    uint64_t *po = A.out.limbs + e * A.out.stride;
+    uint32_t *dout = A.out.degree + e * L;
+
+    for (uint32_t k = lane; k < kMfmaHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
+    wsync();
+    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    uint32_t offo = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        // s_i = x_i ^ carry_i (common.rs:43-47), x_i from the prep workspace
+        store_sum_x(Xg + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
+                    A.status);
+        offo += cap_of(A.ob.b[i]);
+        if (i + 1 == L) break;
+        const int np = bitwords((int)rfl(degPg[i])), nab = bitwords((int)rfl(degABg[i]));
+        const uint32_t *abi = ABg + (size_t)i * A.cntAB;
+        wsync(); // the sum bit's reads of C precede the carry update
+        if (np == 0 || nc == 0) {
+            // P_i * carry_i = 0: carry_{i+1} = ab_i, stale words above it cleared
+            const int n = max(nc, nab);
+            for (int w = lane; w < n; w += kWave) C[w] = w < nab ? abi[w] : 0u;
+            nc = nab;
+            wsync();
+            continue;
+        }
+        // P_i at Pst[kPstLow ..], zeros below and above
+        const uint32_t *pi = Pg + (size_t)i * A.cntP;
+        Pst[lane] = (lane >= kPstLow && lane - kPstLow < np) ? pi[lane - kPstLow] : 0u;
+        // ab_i words of this lane's columns in tiles 0 and 1 (ab_i < 64 words: host plan)
+        const uint32_t ab0 = col < nab ? abi[col] : 0u;
+        const uint32_t ab1 = col + 32 < nab ? abi[col + 32] : 0u;
+        wsync();
+        // All kMfmaChunks chunks run whatever np is: chunks past floor(np/2) have all-zero A (their
+        // P indices are negative), so the chunk loop has no branches and its reads can be issued
+        // ahead of the MFMAs.
+        const int D = np;
+        // A fragments: lane (row m = col, half h), chunk c holds P[s - e], s = 32(D-2c-h) + m
+        v8i Af[kMfmaChunks];
+#pragma unroll
+        for (int c = 0; c < kMfmaChunks; ++c) {
+            const int lo = 32 * (D - 2 * c - h) + col - 31; // window P[lo .. lo+31], lo >= -32*26
+            const int wi = lo >> 5;                           // floor
+            const uint32_t win = funnel(Pst[wi + kPstLow + 1], Pst[wi + kPstLow], (uint32_t)lo & 31u);
+            const uint32_t R = __builtin_bitreverse32(win); // bit e = P[s - e]
+            Af[c] = (v8i){(int)tab[R & 0xFFu], (int)tab[(R >> 8) & 0xFFu],
+                          (int)tab[(R >> 16) & 0xFFu], (int)tab[R >> 24], 0, 0, 0, 0};
+        }
+        const int nout = max(nc + np, nab);
+        const int tiles = (nout + 31) >> 5;
+        ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64);
+        int ldeg = -1;
+        for (int T = tiles - 1; T >= 0; --T) {
+            wsync(); // ring images of this tile's window are written
+            v16f acc;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[j] = 8388608.0f; // 2^23: bit 0 of the f32 = parity
+            // window words 32T + col - D + h + 2c: one base slot, chunk c at +2c slots (32 B)
+            const uint4 *rb = (const uint4 *)&ring[((32 * T + col - D + h) & (kMfmaRingSlots - 1)) * 4];
+            acc = tile_mfma(Af, rb, acc);
+            // the next tile's new window words (still the old carry: they lie below 32T)
+            if (T > 0) ring_fill(C, ring, tab, 32 * (T - 1) - D, 32);
+            // rows (j&3) + 8(j>>2) + 4h of column col: gather bit 0 of each accumulator
+            uint32_t g = 0u;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) g = funnel(__float_as_uint(acc[j]), g, 1);
+            g >>= 16; // bit j = row (j&3) + 8(j>>2) + 4h
+            uint32_t t = (g | (g << 8)) & 0x00FF00FFu;
+            t = ((t | (t << 4)) & 0x0F0F0F0Fu) << (4 * h);
+            const uint32_t word = t | (uint32_t)__shfl_xor((int)t, 32, 64);
+            const int W = 32 * T + col;
+            const uint32_t v = word ^ (T == 0 ? ab0 : T == 1 ? ab1 : 0u);
+            if (h == 0) C[W] = v;
+            if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
+        }
+        const int deg = wave_max_i32(ldeg);
+        nc = deg >= 0 ? (deg >> 5) + 1 : 0;
+        wsync();
+    }
+}
+
+int launch_add_chain_mfma(const AddArgs &a, void *stream) {
+    const int wpb = kAddWavesPerBlock;
+    const uint64_t blocks = (a.n + wpb - 1) / wpb;
+    const size_t lds = (256 + (size_t)a.chain_lds * wpb) * 4;
+    hipLaunchKernelGGL(add_chain_mfma_kernel, dim3((unsigned)blocks), dim3(64 * wpb), lds,
+                       (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace hm

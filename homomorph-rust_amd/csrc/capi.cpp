@@ -402,6 +402,12 @@ hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, ui
     return HM_OK;
 }
 
+hm_status hm_ctx_set_add_options(hm_ctx *c, uint32_t chain) {
+    if (!c || chain > HM_ADD_CHAIN_VALU) return HM_ERR_INVALID_ARGUMENT;
+    c->add_chain = chain;
+    return HM_OK;
+}
+
 hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) {
     if (!c || (ka_min && (ka_leaf < 32 || ka_leaf > 384))) return HM_ERR_INVALID_ARGUMENT;
     c->ka_min = ka_min;
@@ -639,6 +645,18 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     A.chain_lds = A.staged ? staged_lds : even(2 * (A.cw + kHalo) + (L - 1) * cntP);
     A.max_prod_words = SC;
     if ((size_t)A.chain_lds * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
+    // MFMA chain (adder_mfma.hip): P_i within 2*kMfmaChunks-1 words and ab_i within 64 words (two
+    // tiles); carry bits for every tile plus the 64-word window overhang of the ring fill
+    {
+        const uint32_t tiles = (SC + 31) / 32;
+        const uint32_t mf_cw = 32 * tiles + 64;
+        const uint32_t mf_lds = kMfmaHalo + mf_cw + 8 * kMfmaRingSlots + 64;
+        const bool fits = maxPw <= 2 * kMfmaChunks - 1 && cntAB <= 64 &&
+                          (256 + (size_t)mf_lds * kAddWavesPerBlock) * 4 <= 160 * 1024;
+        A.mfma = fits && c->add_chain != HM_ADD_CHAIN_VALU;
+        if (c->add_chain == HM_ADD_CHAIN_MFMA && !fits) return HM_ERR_UNSUPPORTED;
+        if (A.mfma) A.mf_cw = mf_cw, A.chain_lds = mf_lds;
+    }
     A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
     const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
     DeviceGuard g(c->device);

@@ -92,6 +92,31 @@ __device__ __forceinline__ int store_xor_bit(const uint32_t *X, int nx, const ui
     return deg;
 }
 
+// s = X ^ C for the adder's sum bit (x_i from the prep workspace, carry words C); writes the
+// output limbs and the exact degree.
+__device__ __forceinline__ int store_sum_x(const uint32_t *X, int nx, const uint32_t *C, int nc,
+                           uint64_t *__restrict__ dst, uint32_t bound, uint32_t *deg_out,
+                           int *status) {
+    const int lane = lane_id();
+    const int cap = (int)cap_of(bound);
+    const int total = max(cap, (max(nx, nc) + 1) / 2);
+    int ldeg = -1;
+    for (int g = lane; g < total; g += kWave) {
+        const int w = 2 * g;
+        const uint32_t lo = (w < nx ? X[w] : 0u) ^ (w < nc ? C[w] : 0u);
+        const uint32_t hi = (w + 1 < nx ? X[w + 1] : 0u) ^ (w + 1 < nc ? C[w + 1] : 0u);
+        const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (g < cap) dst[g] = v;
+        if (v) ldeg = g * 64 + 63 - __builtin_clzll(v);
+    }
+    const int deg = wave_max_i32(ldeg);
+    if (lane == 0) {
+        if (deg > (int)bound) flag(status, HM_ERR_CAPACITY);
+        *deg_out = (uint32_t)max(deg, 0);
+    }
+    return deg;
+}
+
 __device__ __forceinline__ int words_of(int deg) { return deg >= 0 ? nwords(deg) : 0; }
 
 // dst (cap limbs) = A ^ B ^ C (output bit of the adder); writes the exact degree.

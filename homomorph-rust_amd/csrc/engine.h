@@ -40,6 +40,8 @@ struct AddArgs {
     uint32_t cw;                      // chain: carry buffer words
     uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
     uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)
+    uint32_t mfma;                    // chain on the matrix cores (adder_mfma.hip)
+    uint32_t mf_cw;                   // MFMA chain: carry bit words (tiles, window overhang)
     int *status;
     Bounds ab, bb, ob;
 };
@@ -219,6 +221,7 @@ struct RandArgs {
 // host-side launchers (kernels.hip)
 int launch_random(const RandArgs &a, void *stream);
 int launch_add(const AddArgs &a, void *stream);
+int launch_add_chain_mfma(const AddArgs &a, void *stream);
 int launch_encrypt(const EncArgs &a, void *stream);
 int launch_decrypt(const DecArgs &a, void *stream);
 int launch_gate(const GateArgs &a, void *stream);
@@ -237,6 +240,11 @@ int launch_poly_mul(const PolyArgs &a, void *stream);
 int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
+// MFMA carry chain (adder_mfma.hip): P_i within 2*kMfmaChunks-1 words, nibble ring slots (a power
+// of two above the 58-word window of a tile plus the 32 words filled ahead), zero words below C
+constexpr int kMfmaChunks = 13;
+constexpr int kMfmaRingSlots = 128;
+constexpr int kMfmaHalo = 32;
 constexpr size_t kEncTableBytes = 96 * 1024; // largest encryption nibble table staged in LDS
                                               // (tau = 256 at d + dp = 512: 80 KB)
 

@@ -428,6 +428,16 @@ class Context:
                               "(run more warm-up calls)")
         return EngineGraph(self, g, gen)
 
+    ADD_CHAINS = {"auto": 0, "mfma": 1, "valu": 2}
+
+    def set_add_options(self, chain: str = "auto"):
+        """hm_ctx_set_add_options: where the adder's carry products run -- "mfma" (fp4 matrix
+        cores, a {0,1} Toeplitz product reduced mod 2), "valu" (scalar-decided XORs) or "auto"
+        (MFMA when the plan fits).  Results are identical either way (every product is exact);
+        "mfma" on a plan it cannot run makes the add raise EngineError (HM_ERR_UNSUPPORTED)."""
+        _check(lib().hm_ctx_set_add_options(self._h, self.ADD_CHAINS[chain]),
+               "hm_ctx_set_add_options")
+
     def set_mul_options(self, karatsuba_min_words: int = 1024, karatsuba_leaf_words: int = 256):
         """hm_ctx_set_mul_options: which carry products of the multiplier run as Karatsuba
         recursions (shorter operand >= karatsuba_min_words words; 0 = never) and their leaf

@@ -71,6 +71,7 @@ SIGNATURES = {
     "hm_ctx_get_public_key": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u32p, u32p]),
     "hm_validate_operation": (ctypes.c_int, [vp, ctypes.c_int, u16p]),
     "hm_ctx_set_mul_options": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "hm_ctx_set_add_options": (ctypes.c_int, [vp, ctypes.c_uint32]),
     "hm_fresh_bound": (ctypes.c_uint32, [vp]),
     "hm_add_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, u32p]),
     "hm_mul_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, ctypes.c_int, u32p]),

@@ -156,6 +156,16 @@ hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
 hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
                                  uint32_t karatsuba_leaf_words);
 
+/* Adder strategy (no effect on results: both chains are exact).  The carry chain
+ * carry' = ab_i ^ P_i * carry (src/impls/numbers/common.rs:37-56) runs its products either on the
+ * matrix cores (a {0,1} Toeplitz product on fp4 MFMA, reduced mod 2; needs P_i within 25 words,
+ * i.e. d + dp <= 256 for u32) or as scalar-decided VALU XORs.  AUTO picks the MFMA chain when it
+ * applies; MFMA on a plan it cannot run returns HM_ERR_UNSUPPORTED at hm_add_batch. */
+#define HM_ADD_CHAIN_AUTO 0u
+#define HM_ADD_CHAIN_MFMA 1u
+#define HM_ADD_CHAIN_VALU 2u
+hm_status hm_ctx_set_add_options(hm_ctx *ctx, uint32_t chain);
+
 /* Context::validate_operation (src/context.rs:310-323): HM_OK or HM_ERR_INVALID_PARAMETERS with
  * the OperationError payload written to *required_min_d_over_delta (may be NULL). */
 hm_status hm_validate_operation(const hm_ctx *ctx, hm_op op, uint16_t *required_min_d_over_delta);

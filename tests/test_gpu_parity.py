@@ -155,6 +155,7 @@ def _pair(H, ctx, params, dtype, n, seed, lo=None, hi=None):
     return a, b, ma, mb, ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb)
 
 
+@pytest.mark.parametrize("chain", ["auto", "valu"])
 @pytest.mark.parametrize("params,dtype,n", [((64, 64, 1, 64), np.uint8, 128),
                                             ((64, 64, 1, 64), np.uint32, 32),
                                             ((64, 16, 1, 16), np.uint8, 64),
@@ -162,9 +163,12 @@ def _pair(H, ctx, params, dtype, n, seed, lo=None, hi=None):
                                             ((128, 128, 4, 128), np.uint16, 32),
                                             ((256, 256, 1, 256), np.uint32, 4),
                                             ((256, 128, 1, 128), np.uint64, 2)])
-def test_add_parity(H, oracle, params, dtype, n):
+def test_add_parity(H, oracle, params, dtype, n, chain):
+    """Both carry chains (fp4 MFMA Toeplitz products and VALU XORs) against the oracle.  "auto"
+    runs the MFMA chain wherever P_i fits 25 words (d + dp <= 256 here), the VALU chain above."""
     d, dp, delta, tau = params
     ctx = make_ctx(H, params, 17)
+    ctx.set_add_options(chain)
     sk, pk, _ = keys(*params, 17)
     a, b, ma, mb, ca, cb = _pair(H, ctx, params, dtype, n, 18)
     cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
@@ -187,10 +191,13 @@ def test_add_parity(H, oracle, params, dtype, n):
         assert np.array_equal(dec, (a + b).astype(dtype))
 
 
-def test_add_edge_values(H, oracle):
-    """Wrap-around and extremes (uint.rs:202-208: 255 + 240 = 239), zero, all-ones."""
+@pytest.mark.parametrize("chain", ["mfma", "valu"])
+def test_add_edge_values(H, oracle, chain):
+    """Wrap-around and extremes (uint.rs:202-208: 255 + 240 = 239), zero, all-ones; the zero
+    operands give null P_i and null carries (the MFMA chain's copy-ab branch)."""
     params = (128, 128, 1, 128)
     ctx = make_ctx(H, params, 5)
+    ctx.set_add_options(chain)
     sk, pk, _ = keys(*params, 5)
     a = np.array([0, 0xFFFFFFFF, 0xFFFFFFFF, 255, 1, 0x80000000], dtype=np.uint32)
     b = np.array([0, 1, 0xFFFFFFFF, 240, 0, 0x80000000], dtype=np.uint32)
@@ -208,6 +215,17 @@ def test_add_edge_values(H, oracle):
     gl, gd = cs.to_host()
     assert_batches_equal(gl, gd, rl, rd, ob, n, "add edges")
     assert np.array_equal(dec, (a.astype(np.uint64) + b) .astype(np.uint32))
+
+
+def test_add_chain_mfma_unsupported(H):
+    """A forced MFMA chain on a plan whose P_i exceeds 25 words is refused, not approximated."""
+    params = (256, 256, 1, 256)
+    ctx = make_ctx(H, params, 3)
+    ctx.set_add_options("mfma")
+    a = ctx.encrypt(np.array([1, 2], dtype=np.uint8), masks=masks(2, 8, 256, 1))
+    with pytest.raises(H.EngineError):
+        ctx.apply2(H.HomomorphicAddition, a, a)
+        ctx.synchronize()
 
 
 def test_successive_add(H, oracle):

@@ -1,0 +1,138 @@
+// chain_check.hip -- standalone check of the MFMA carry chain (homomorph-rust_amd/csrc/adder_mfma.hip)
+// against a CPU carry-less chain on a synthetic prep workspace:
+//   carry_0 = 0;  s_i = x_i ^ carry_i;  carry_{i+1} = ab_i ^ P_i * carry_i
+// Modes: random words, or single set bits (localises index errors).  Prints the first mismatching
+// output words.  build: hipcc --offload-arch=gfx950 -O3 -I homomorph-rust_amd/csrc \
+//   tools/chain_check.hip -o tools/chain_check
+#include "../homomorph-rust_amd/csrc/adder_mfma.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+using namespace hm;
+
+static std::vector<uint32_t> clmul(const std::vector<uint32_t> &a, const std::vector<uint32_t> &b) {
+    std::vector<uint32_t> r(a.size() + b.size() + 1, 0u);
+    for (size_t i = 0; i < a.size() * 32; ++i)
+        if ((a[i / 32] >> (i % 32)) & 1u)
+            for (size_t j = 0; j < b.size() * 32; ++j)
+                if ((b[j / 32] >> (j % 32)) & 1u) r[(i + j) / 32] ^= 1u << ((i + j) % 32);
+    return r;
+}
+static int degp1(const uint32_t *w, int n) {
+    for (int k = n - 1; k >= 0; --k)
+        if (w[k]) return k * 32 + 32 - __builtin_clz(w[k]);
+    return 0;
+}
+
+static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool quiet);
+
+int main(int argc, char **argv) {
+    if (argc > 1 && !strcmp(argv[1], "sweep")) {
+        const int ps[] = {0, 5, 31, 32, 100, 400, 650, 700, 736, 767};
+        const int cs[] = {0, 7, 31, 32, 100, 300, 480, 511};
+        int nbad = 0;
+        for (int pb : ps)
+            for (int cb : cs)
+                if (run_case(3, 24, 16, 1, pb, cb, true)) {
+                    const int o = pb + cb;
+                    printf("FAIL p=%d c=%d -> out bit %d (W=%d m=%d, cword=%d, pword=%d)\n", pb, cb, o, o / 32, o % 32, cb / 32, pb / 32);
+                    ++nbad;
+                }
+        printf("sweep: %d failing cases\n", nbad);
+        return 0;
+    }
+    const int L = argc > 1 ? atoi(argv[1]) : 4;          // bits
+    const int npw = argc > 2 ? atoi(argv[2]) : 24;       // P words
+    const int abw = argc > 3 ? atoi(argv[3]) : 16;       // ab words
+    const int mode = argc > 4 ? atoi(argv[4]) : 0;       // 0 random, 1 single bits
+    const int pbit = argc > 5 ? atoi(argv[5]) : 0, cbit = argc > 6 ? atoi(argv[6]) : 0;
+    return run_case(L, npw, abw, mode, pbit, cbit, false) ? 1 : 0;
+}
+
+static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool quiet) {
+    std::mt19937_64 rng(5);
+    const uint32_t cntAB = abw, cntP = npw, cntX = 9;
+    std::vector<std::vector<uint32_t>> P(L), AB(L), X(L);
+    for (int i = 0; i < L; ++i) {
+        P[i].assign(cntP, 0u), AB[i].assign(cntAB, 0u), X[i].assign(cntX, 0u);
+        if (mode == 0) {
+            for (auto &w : P[i]) w = (uint32_t)rng();
+            for (auto &w : AB[i]) w = (uint32_t)rng();
+        } else {
+            P[i][pbit / 32] = 1u << (pbit % 32);
+            if (i == 0) AB[i][cbit / 32] = 1u << (cbit % 32);
+        }
+    }
+    // CPU chain
+    std::vector<std::vector<uint32_t>> S(L);
+    std::vector<uint32_t> carry;
+    size_t maxw = 0;
+    for (int i = 0; i < L; ++i) {
+        S[i] = carry;
+        if (S[i].size() < cntX) S[i].resize(cntX, 0u);
+        for (uint32_t k = 0; k < cntX; ++k) S[i][k] ^= X[i][k];
+        maxw = std::max(maxw, S[i].size());
+        auto pr = clmul(P[i], carry);
+        pr.resize(std::max(pr.size(), (size_t)cntAB), 0u);
+        for (uint32_t k = 0; k < cntAB; ++k) pr[k] ^= AB[i][k];
+        carry = pr;
+    }
+    // workspace
+    AddArgs A{};
+    A.n = 1, A.nbits = L, A.cntAB = cntAB, A.cntP = cntP, A.cntX = cntX;
+    A.ws_stride = (uint64_t)L * (cntAB + cntP + 2 + cntX);
+    std::vector<uint32_t> ws(A.ws_stride, 0u);
+    for (int i = 0; i < L; ++i) {
+        memcpy(&ws[i * cntAB], AB[i].data(), cntAB * 4);
+        memcpy(&ws[L * cntAB + i * cntP], P[i].data(), cntP * 4);
+        ws[L * (cntAB + cntP) + i] = degp1(AB[i].data(), cntAB);
+        ws[L * (cntAB + cntP) + L + i] = degp1(P[i].data(), cntP);
+        memcpy(&ws[L * (cntAB + cntP + 2) + i * cntX], X[i].data(), cntX * 4);
+    }
+    uint32_t outcap = (uint32_t)((maxw * 32 + 63) / 64 + 1);
+    for (int i = 0; i < L; ++i) A.ob.b[i] = outcap * 64 - 1;
+    A.out.stride = (uint64_t)outcap * L;
+    const uint32_t tiles = (uint32_t)((maxw + 31) / 32) + 1;
+    A.mf_cw = 32 * tiles + 64;
+    A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + 64;
+    A.mfma = 1;
+    uint32_t *dws;
+    uint64_t *dout;
+    uint32_t *ddeg;
+    int *dst;
+    hipMalloc(&dws, ws.size() * 4);
+    hipMalloc(&dout, A.out.stride * 8);
+    hipMalloc(&ddeg, L * 4);
+    hipMalloc(&dst, 4);
+    hipMemcpy(dws, ws.data(), ws.size() * 4, hipMemcpyHostToDevice);
+    hipMemset(dout, 0, A.out.stride * 8);
+    hipMemset(dst, 0, 4);
+    A.ws = dws, A.out.limbs = dout, A.out.degree = ddeg, A.status = dst;
+    if (launch_add_chain_mfma(A, nullptr)) { printf("launch failed\n"); return 2; }
+    hipDeviceSynchronize();
+    std::vector<uint64_t> out(A.out.stride);
+    hipMemcpy(out.data(), dout, out.size() * 8, hipMemcpyDeviceToHost);
+    int st;
+    hipMemcpy(&st, dst, 4, hipMemcpyDeviceToHost);
+    int bad = 0;
+    for (int i = 0; i < L; ++i) {
+        const uint32_t *g = (const uint32_t *)&out[(size_t)i * outcap];
+        int shown = 0;
+        for (size_t k = 0; k < 2 * outcap; ++k) {
+            const uint32_t ref = k < S[i].size() ? S[i][k] : 0u;
+            if (g[k] != ref) {
+                ++bad;
+                if (!quiet && shown++ < 6) printf("bit %d word %zu: gpu %08x ref %08x\n", i, k, g[k], ref);
+            }
+        }
+    }
+    if (!quiet)
+        printf("L=%d np=%d ab=%d mode=%d pbit=%d cbit=%d: %d mismatching words, status %d\n", L, npw,
+               abw, mode, pbit, cbit, bad, st);
+    hipFree(dws), hipFree(dout), hipFree(ddeg), hipFree(dst);
+    return bad;
+}
