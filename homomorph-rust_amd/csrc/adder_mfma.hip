@@ -27,7 +27,7 @@
 //         top (tile T's output words are no longer read by tiles < T);
 //   ring  nibble images of the carry words the next tiles read (fp4 1.0 per set bit, 16 B per
 //         word, 128 slots mapped twice): a B fragment is one ds_read_b128;
-//   Pst   P_i above kPstLow zero words (the A windows of the chunks past P reach P word -26).
+//   RS    the nibble image of P_i bit-reversed: an A fragment is a 128-bit window of it.
 // A 1 KB table per block maps a byte to its 8 nibbles.
 //
 // Parity: every accumulator starts at 2^23, so after the MFMAs it holds 2^23 + count exactly and
@@ -39,7 +39,11 @@
 namespace hm {
 
 typedef int v8i __attribute__((ext_vector_type(8)));
-constexpr int kPstLow = 28; // zero words below P_i in Pst (64 words: P_i within 25, zeros above)
+// RS: P_i bit-reversed over kRevWords words (> 25), as nibble words, plus the zero nibble words
+// that the windows of the chunks past P reach (j0 + 31 < 32*kRevWords + 32*26)
+constexpr int kRevWords = 28;
+constexpr int kRsWords = 4 * kRevWords + 4 * 26 + 8;
+static_assert(kRsWords <= kMfmaRsWords, "engine.h kMfmaRsWords");
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
@@ -103,11 +107,11 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
     const int lane = lane_id();
     const int col = lane & 31, h = lane >> 5;
     const uint32_t L = A.nbits;
-    // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][Pst: 64]
+    // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][RS: kRsWords]
     uint32_t *Ls = lds + 256 + (size_t)wave * A.chain_lds;
     uint32_t *C = Ls + kMfmaHalo;
     uint32_t *ring = C + A.mf_cw;
-    uint32_t *Pst = ring + 8 * kMfmaRingSlots;
+    uint32_t *RS = ring + 8 * kMfmaRingSlots;
     const uint32_t *ws = A.ws + e * A.ws_stride;
     const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
     const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
@@ -115,6 +119,7 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
     uint32_t *dout = A.out.degree + e * L;
 
     for (uint32_t k = lane; k < kMfmaHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
+    for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u; // P below bit 0
     wsync();
     int nc = 0; // carry words (0 = null carry, common.rs:39)
     uint32_t offo = 0;
@@ -135,9 +140,14 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             wsync();
             continue;
         }
-        // P_i at Pst[kPstLow ..], zeros below and above
+        // RS = nibble image of P_i bit-reversed over kRevWords words: nibble j = P[32*kRevWords-1-j]
+        // (nibble words >= 4*kRevWords stay zero: P below bit 0).
         const uint32_t *pi = Pg + (size_t)i * A.cntP;
-        Pst[lane] = (lane >= kPstLow && lane - kPstLow < np) ? pi[lane - kPstLow] : 0u;
+        for (int k = lane; k < 4 * kRevWords; k += kWave) {
+            const int q = kRevWords - 1 - (k >> 2); // the P word behind nibble word k
+            const uint32_t rev = __builtin_bitreverse32(q < np ? pi[q] : 0u);
+            RS[k] = tab[(rev >> (8 * (k & 3))) & 0xFFu];
+        }
         // ab_i words of this lane's columns in tiles 0 and 1 (ab_i < 64 words: host plan)
         const uint32_t ab0 = col < nab ? abi[col] : 0u;
         const uint32_t ab1 = col + 32 < nab ? abi[col + 32] : 0u;
@@ -146,26 +156,31 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
         // P indices are negative), so the chunk loop has no branches and its reads can be issued
         // ahead of the MFMAs.
         const int D = np;
-        // A fragments: lane (row m = col, half h), chunk c holds P[s - e], s = 32(D-2c-h) + m
+        // A fragments: lane (row m = col, half h), chunk c holds P[s - e], s = 32(D-2c-h) + m,
+        // i.e. RS nibbles j0 .. j0+31 with j0 = 32*kRevWords - 1 - s: five words, four funnels
         v8i Af[kMfmaChunks];
 #pragma unroll
         for (int c = 0; c < kMfmaChunks; ++c) {
-            const int lo = 32 * (D - 2 * c - h) + col - 31; // window P[lo .. lo+31], lo >= -32*26
-            const int wi = lo >> 5;                           // floor
-            const uint32_t win = funnel(Pst[wi + kPstLow + 1], Pst[wi + kPstLow], (uint32_t)lo & 31u);
-            const uint32_t R = __builtin_bitreverse32(win); // bit e = P[s - e]
-            Af[c] = (v8i){(int)tab[R & 0xFFu], (int)tab[(R >> 8) & 0xFFu],
-                          (int)tab[(R >> 16) & 0xFFu], (int)tab[R >> 24], 0, 0, 0, 0};
+            const int j0 = 32 * kRevWords - 1 - (32 * (D - 2 * c - h) + col);
+            const uint32_t *rw = RS + (j0 >> 3);
+            const uint32_t sh = 4u * (uint32_t)(j0 & 7);
+            const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3], w4 = rw[4];
+            Af[c] = (v8i){(int)funnel(w1, w0, sh), (int)funnel(w2, w1, sh), (int)funnel(w3, w2, sh),
+                          (int)funnel(w4, w3, sh), 0, 0, 0, 0};
         }
         const int nout = max(nc + np, nab);
         const int tiles = (nout + 31) >> 5;
         ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64);
         int ldeg = -1;
+        // The accumulators start at 2^23 once per bit and keep accumulating tile after tile
+        // (2^23 + every count stays below 2^24, exact): a tile's parities are bit 0 of its
+        // accumulators XOR bit 0 before the tile.
+        v16f acc;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 8388608.0f;
+        uint32_t gprev = 0u;
         for (int T = tiles - 1; T >= 0; --T) {
             wsync(); // ring images of this tile's window are written
-            v16f acc;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) acc[j] = 8388608.0f; // 2^23: bit 0 of the f32 = parity
             // window words 32T + col - D + h + 2c: one base slot, chunk c at +2c slots (32 B)
             const uint4 *rb = (const uint4 *)&ring[((32 * T + col - D + h) & (kMfmaRingSlots - 1)) * 4];
             acc = tile_mfma(Af, rb, acc);
@@ -175,7 +190,10 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             uint32_t g = 0u;
 #pragma unroll
             for (int j = 0; j < 16; ++j) g = funnel(__float_as_uint(acc[j]), g, 1);
-            g >>= 16; // bit j = row (j&3) + 8(j>>2) + 4h
+            g >>= 16;
+            const uint32_t gnow = g;
+            g ^= gprev; // bit j = row (j&3) + 8(j>>2) + 4h
+            gprev = gnow;
             uint32_t t = (g | (g << 8)) & 0x00FF00FFu;
             t = ((t | (t << 4)) & 0x0F0F0F0Fu) << (4 * h);
             const uint32_t word = t | (uint32_t)__shfl_xor((int)t, 32, 64);

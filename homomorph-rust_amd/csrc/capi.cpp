@@ -650,7 +650,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     {
         const uint32_t tiles = (SC + 31) / 32;
         const uint32_t mf_cw = 32 * tiles + 64;
-        const uint32_t mf_lds = kMfmaHalo + mf_cw + 8 * kMfmaRingSlots + 64;
+        const uint32_t mf_lds = kMfmaHalo + mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
         const bool fits = maxPw <= 2 * kMfmaChunks - 1 && cntAB <= 64 &&
                           (256 + (size_t)mf_lds * kAddWavesPerBlock) * 4 <= 160 * 1024;
         A.mfma = fits && c->add_chain != HM_ADD_CHAIN_VALU;

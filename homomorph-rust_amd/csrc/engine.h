@@ -245,6 +245,7 @@ constexpr int kAddWavesPerBlock = 4;
 constexpr int kMfmaChunks = 13;
 constexpr int kMfmaRingSlots = 128;
 constexpr int kMfmaHalo = 32;
+constexpr int kMfmaRsWords = 224; // reversed nibble image of P_i (adder_mfma.hip kRsWords)
 constexpr size_t kEncTableBytes = 96 * 1024; // largest encryption nibble table staged in LDS
                                               // (tau = 256 at d + dp = 512: 80 KB)
 

@@ -98,7 +98,7 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     A.out.stride = (uint64_t)outcap * L;
     const uint32_t tiles = (uint32_t)((maxw + 31) / 32) + 1;
     A.mf_cw = 32 * tiles + 64;
-    A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + 64;
+    A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
     A.mfma = 1;
     uint32_t *dws;
     uint64_t *dout;
