@@ -16,7 +16,8 @@ WORLD_SIZE equals N.  `--workload distcheck` runs only the multi-rank plumbing (
 broadcast, shards, result gather, max-over-ranks time) on the CPU with gloo, for the CPU tests.
 
 Prints ONE JSON line (rank 0).  Besides the contract fields it carries
-  roofline      HBM roofline of the add kernel: algorithmic bytes per launch / kernel time
+  roofline      MFMA roofline of the dominant kernel (the carry chain on fp4 matrix cores):
+                algorithmic bit-pair ops per launch / its HIP-event duration, vs the dense fp4 peak
   cpu_baseline  the CPU oracle (operation-for-operation restatement of the reference) timed on a
                 bounded sample on this host: one thread (the reference is single-threaded) and
                 all host cores (values split over OpenMP threads), CPU model stated
@@ -46,6 +47,21 @@ PARAMS = (128, 128, 1, 128)
 MUL_LOW_BENCH = 16  # configs[3]: result bits of the u32 multiply that are run
 BENCH_SEED = 0xB0B  # rank 0's keys and the mask stream (hm_ctx_seed_rng, the test contract)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP4_MFMA_PEAK_TFLOPS = 10000.0  # MI355X dense FP4 MFMA peak (MI355X_MICROARCH.md; not the sparse 20 PF)
+
+
+def chain_bit_pairs(ba, bb):
+    """Schoolbook bit pairs of the adder chain's carry products (common.rs:37-56 as carry' =
+    ab_i ^ P_i * carry_i): sum over bits i = 1 .. L-2 of (deg P_i + 1) * (deg carry_i + 1) at the
+    static degree bounds, deg P_i <= max(a_i, b_i) + a_i + b_i and deg carry_{i+1} <= deg P_i +
+    deg carry_i with carry_1 = a_0 b_0.  Bit 0 multiplies a null carry, bit L-1 has no carry out."""
+    ba, bb = [int(x) for x in ba], [int(x) for x in bb]
+    total, carry = 0, ba[0] + bb[0]
+    for i in range(1, len(ba) - 1):
+        p = max(ba[i], bb[i]) + ba[i] + bb[i]
+        total += (p + 1) * (carry + 1)
+        carry = max(ba[i] + bb[i], p + carry)
+    return total
 
 
 def log(*a):
@@ -428,9 +444,23 @@ def run_add(args, world, rank, device):
     if args.graph:  # the step as one captured HIP graph (prep + chain), replayed per step
         g = ctx.graph(lambda: H.add_into(ctx, ca, cb, out))
         wall, ev_s = time_loop(g.replay, args.steps, args.warmup, world)
+        # a graph replay cannot carry per-launch events: the chain kernel is timed over the same
+        # number of direct launches right after the timed region
+        ctx.set_kernel_timing(True)
+        for _ in range(args.steps):
+            H.add_into(ctx, ca, cb, out)
+        chain_ms, chain_n = ctx.kernel_timing()
+        ctx.set_kernel_timing(False)
+        chain_src = f"HIP events around each chain launch on the engine stream, {chain_n} direct launches after the timed graph replays"
     else:
-        wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, args.warmup,
-                               world, ctx.stream)
+        for _ in range(args.warmup):
+            H.add_into(ctx, ca, cb, out)
+        ctx.set_kernel_timing(True)  # events around every chain launch of the timed region
+        wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, 0, world,
+                               ctx.stream)
+        chain_ms, chain_n = ctx.kernel_timing()
+        ctx.set_kernel_timing(False)
+        chain_src = f"HIP events around each of the timed region's {chain_n} chain launches (engine stream)"
     ctx.synchronize()  # raises on any device-side error flag
     # verification (untimed): decrypt on device, gather the plaintexts over RCCL, check on rank 0
     got, wall = gather_results(world, device, ctx.decrypt_bytes(out), wall)
@@ -443,7 +473,9 @@ def run_add(args, world, rank, device):
     out_bytes = 8 * out.stride
     per_add = in_bytes + out_bytes
     kernel_s = ev_s / args.steps
-    achieved = n * per_add / kernel_s / 1e9
+    chain_s = chain_ms / 1e3 / max(1, chain_n)
+    pairs = chain_bit_pairs(ca.bound, cb.bound)
+    achieved = 2.0 * pairs * n / chain_s / 1e12  # TFLOP/s: one bit-pair AND+XOR = one MAC = 2 ops
     traffic = None
     try:
         with open(args.traffic) as f:
@@ -470,11 +502,16 @@ def run_add(args, world, rank, device):
                    "batch_per_gpu": n, "d": PARAMS[0], "dp": PARAMS[1], "delta": PARAMS[2],
                    "tau": PARAMS[3], "parallelism": f"batch-sharded x{world}"},
         "verified": {"correct_sums": correct, "of": n * world},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": 1e3 * kernel_s, "alg_bytes_per_add": per_add,
-                     "kernels": "add_prep_kernel + add_chain_staged_kernel (one launch)",
-                     "note": "issue-bound (VALU + scalar bit decisions), not HBM: DESIGN.md s4"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP4_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / FP4_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "add_chain_mfma_kernel (carry products as {0,1} Toeplitz GEMMs on "
+                               "fp4 MFMA)",
+                     "kernel_ms": 1e3 * chain_s, "kernel_ms_source": chain_src,
+                     "alg_bit_pairs_per_add": pairs, "step_kernels_ms": 1e3 * kernel_s,
+                     "hbm_gbs_step": n * per_add / kernel_s / 1e9, "alg_bytes_per_add": per_add,
+                     "note": "algorithmic work = schoolbook bit pairs of the chain's carry products "
+                             "P_i * carry_i over the static degree bounds (DESIGN.md s4.1); "
+                             "traffic = PMC HBM bytes of one add step (prep + chain)"},
     }
     if rank == 0 and world == 1 and not args.no_secondary:
         try:

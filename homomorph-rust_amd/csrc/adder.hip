@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
     }
 }
 
-int launch_add(const AddArgs &a, void *stream) {
+int launch_add(const AddArgs &a, void *stream, void *ev0, void *ev1) {
     if (a.n == 0) return 0;
     // prep: wpv waves per value, 4 waves per block
     {
@@ -295,7 +295,15 @@ int launch_add(const AddArgs &a, void *stream) {
                            (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    if (a.mfma) return launch_add_chain_mfma(a, stream);
+    if (ev0 && hipEventRecord((hipEvent_t)ev0, (hipStream_t)stream) != hipSuccess) return -1;
+    int rc = 0;
+    if (a.mfma) rc = launch_add_chain_mfma(a, stream);
+    else rc = launch_add_chain_valu(a, stream);
+    if (ev1 && hipEventRecord((hipEvent_t)ev1, (hipStream_t)stream) != hipSuccess) return -1;
+    return rc;
+}
+
+int launch_add_chain_valu(const AddArgs &a, void *stream) {
     const int wpb = kAddWavesPerBlock;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     const size_t lds = (size_t)a.chain_lds * 4 * wpb;

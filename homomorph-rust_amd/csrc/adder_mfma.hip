@@ -46,6 +46,17 @@ constexpr int kRsWords = 4 * kRevWords + 4 * 26 + 8;
 static_assert(kRsWords <= kMfmaRsWords, "engine.h kMfmaRsWords");
 typedef float v16f __attribute__((ext_vector_type(16)));
 
+// Phase timers (tools/chain_check.hip builds with HM_MFMA_PROFILE; the library never does):
+// per-wave sums of s_memtime deltas for the sum store, the A build and the tile loop.
+#ifdef HM_MFMA_PROFILE
+__device__ unsigned long long *g_mfma_prof; // 4 per wave, set by the harness
+#define HM_PT(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define HM_PACC(k, a, b) prof[k] += (b) - (a)
+#else
+#define HM_PT(v)
+#define HM_PACC(k, a, b)
+#endif
+
 __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
     // cbsz = blgp = 4: both operands fp4 e2m1; E8M0 scales 127 = 1.0
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
@@ -93,6 +104,7 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
 
 __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
+    __shared__ uint32_t stage[kAddWavesPerBlock][2][64];
     uint32_t *tab = lds; // byte -> 8 nibbles, fp4 1.0 (0b0010) per set bit
     for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
         uint32_t v = 0u;
@@ -117,20 +129,55 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
     const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
     uint64_t *po = A.out.limbs + e * A.out.stride;
     uint32_t *dout = A.out.degree + e * L;
+    // Bit i's workspace record, copied into stage[wave][i&1] by one LDS-DMA a bit ahead (its
+    // latency hides behind the previous bit's tiles): [x_i: cntX][P_i: cntP][ab_i: cntAB][deg P_i]
+    // [deg ab_i] (host plan: at most 64 words).  The DMA is asm: the compiler cannot tell the
+    // dynamic LDS from stage and would wait for the DMA before the next LDS write; instead each
+    // bit starts with one vmcnt(0), when the DMA and the previous bit's stores are a bit old.
+    const uint32_t oP = A.cntX, oAB = oP + A.cntP, oD = oAB + A.cntAB;
+    // lane l's record word of bit i is workspace word lbase + i * lstep (lanes past the record
+    // re-read deg P_i)
+    uint32_t lbase, lstep;
+    {
+        const uint32_t ul = (uint32_t)lane, offD = L * (A.cntAB + A.cntP);
+        if (ul < oP) lbase = offD + 2 * L + ul, lstep = A.cntX;
+        else if (ul < oAB) lbase = L * A.cntAB + (ul - oP), lstep = A.cntP;
+        else if (ul < oD) lbase = ul - oAB, lstep = A.cntAB;
+        else if (ul == oD + 1) lbase = offD, lstep = 1;
+        else lbase = offD + L, lstep = 1;
+    }
+    const uint64_t wsu = ((uint64_t)rfl((uint32_t)((uintptr_t)ws >> 32)) << 32) |
+                         rfl((uint32_t)(uintptr_t)ws); // wave-uniform: SGPR base of the DMA
+    auto stage_rec = [&](uint32_t i) {
+        const uint32_t voff = 4u * (lbase + i * lstep);
+        const uint32_t m0 = (uint32_t)(uintptr_t)&stage[wave][i & 1][0]; // LDS byte offset
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                     :
+                     : "v"(voff), "s"(wsu), "s"(m0)
+                     : "memory", "m0");
+    };
+    stage_rec(0);
 
+#ifdef HM_MFMA_PROFILE
+    unsigned long long prof[3] = {0, 0, 0};
+#endif
     for (uint32_t k = lane; k < kMfmaHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
     for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u; // P below bit 0
     wsync();
     int nc = 0; // carry words (0 = null carry, common.rs:39)
     uint32_t offo = 0;
     for (uint32_t i = 0; i < L; ++i) {
-        // s_i = x_i ^ carry_i (common.rs:43-47), x_i from the prep workspace
-        store_sum_x(Xg + (size_t)i * A.cntX, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i,
-                    A.status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
+        const uint32_t *rec = &stage[wave][i & 1][0];
+        // s_i = x_i ^ carry_i (common.rs:43-47)
+        HM_PT(t0);
+        store_sum_x(rec, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
         offo += cap_of(A.ob.b[i]);
+        HM_PT(t1);
+        HM_PACC(0, t0, t1);
         if (i + 1 == L) break;
-        const int np = bitwords((int)rfl(degPg[i])), nab = bitwords((int)rfl(degABg[i]));
-        const uint32_t *abi = ABg + (size_t)i * A.cntAB;
+        const int np = bitwords((int)rfl(rec[oD])), nab = bitwords((int)rfl(rec[oD + 1]));
+        const uint32_t *abi = rec + oAB;
         wsync(); // the sum bit's reads of C precede the carry update
         if (np == 0 || nc == 0) {
             // P_i * carry_i = 0: carry_{i+1} = ab_i, stale words above it cleared
@@ -138,20 +185,20 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             for (int w = lane; w < n; w += kWave) C[w] = w < nab ? abi[w] : 0u;
             nc = nab;
             wsync();
+            stage_rec(i + 1);
             continue;
         }
         // RS = nibble image of P_i bit-reversed over kRevWords words: nibble j = P[32*kRevWords-1-j]
         // (nibble words >= 4*kRevWords stay zero: P below bit 0).
-        const uint32_t *pi = Pg + (size_t)i * A.cntP;
+        const uint32_t *pi = rec + oP;
         for (int k = lane; k < 4 * kRevWords; k += kWave) {
             const int q = kRevWords - 1 - (k >> 2); // the P word behind nibble word k
             const uint32_t rev = __builtin_bitreverse32(q < np ? pi[q] : 0u);
             RS[k] = tab[(rev >> (8 * (k & 3))) & 0xFFu];
         }
-        // ab_i words of this lane's columns in tiles 0 and 1 (ab_i < 64 words: host plan)
-        const uint32_t ab0 = col < nab ? abi[col] : 0u;
-        const uint32_t ab1 = col + 32 < nab ? abi[col + 32] : 0u;
         wsync();
+        // bit i+1's record goes to the other buffer (this one is read until the last tile)
+        stage_rec(i + 1);
         // All kMfmaChunks chunks run whatever np is: chunks past floor(np/2) have all-zero A (their
         // P indices are negative), so the chunk loop has no branches and its reads can be issued
         // ahead of the MFMAs.
@@ -168,6 +215,8 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             Af[c] = (v8i){(int)funnel(w1, w0, sh), (int)funnel(w2, w1, sh), (int)funnel(w3, w2, sh),
                           (int)funnel(w4, w3, sh), 0, 0, 0, 0};
         }
+        HM_PT(t2);
+        HM_PACC(1, t1, t2);
         const int nout = max(nc + np, nab);
         const int tiles = (nout + 31) >> 5;
         ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64);
@@ -198,14 +247,20 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             t = ((t | (t << 4)) & 0x0F0F0F0Fu) << (4 * h);
             const uint32_t word = t | (uint32_t)__shfl_xor((int)t, 32, 64);
             const int W = 32 * T + col;
-            const uint32_t v = word ^ (T == 0 ? ab0 : T == 1 ? ab1 : 0u);
+            const uint32_t v = word ^ (W < nab ? abi[W] : 0u); // ab_i < 64 words (host plan)
             if (h == 0) C[W] = v;
             if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
         }
         const int deg = wave_max_i32(ldeg);
         nc = deg >= 0 ? (deg >> 5) + 1 : 0;
         wsync();
+        HM_PT(t3);
+        HM_PACC(2, t2, t3);
     }
+#ifdef HM_MFMA_PROFILE
+    if (lane == 0)
+        for (int k = 0; k < 3; ++k) g_mfma_prof[e * 4 + k] = prof[k];
+#endif
 }
 
 int launch_add_chain_mfma(const AddArgs &a, void *stream) {

@@ -268,6 +268,7 @@ void hm_ctx_destroy(hm_ctx *c) {
                     (void *)c->d_masks, (void *)c->d_mws})
         if (p) (void)hipFree(p);
     for (auto &r : c->retired) (void)hipFree(r.p);
+    for (auto &e : c->tev) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     wipe(c->chacha_key, sizeof(c->chacha_key));
     wipe(&c->rng, sizeof(c->rng));
@@ -399,6 +400,33 @@ hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, ui
         if (cap < c->pk.size()) return HM_ERR_CAPACITY;
         std::memcpy(limbs, c->pk.data(), c->pk.size() * 8);
     }
+    return HM_OK;
+}
+
+hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    if (enable && c->tev.empty()) {
+        c->tev.resize(2 * kTimedLaunches);
+        for (auto &e : c->tev) HM_HIP(c, hipEventCreate(&e));
+    }
+    c->time_chain = enable != 0;
+    c->tev_used = 0;
+    return HM_OK;
+}
+
+hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) {
+    if (!c || !total_ms || !launches) return HM_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(c->device);
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    double t = 0.0;
+    for (size_t k = 0; k + 1 < c->tev_used; k += 2) {
+        float ms = 0.0f;
+        HM_HIP(c, hipEventElapsedTime(&ms, c->tev[k], c->tev[k + 1]));
+        t += ms;
+    }
+    *total_ms = t;
+    *launches = (uint32_t)(c->tev_used / 2);
     return HM_OK;
 }
 
@@ -645,13 +673,15 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     A.chain_lds = A.staged ? staged_lds : even(2 * (A.cw + kHalo) + (L - 1) * cntP);
     A.max_prod_words = SC;
     if ((size_t)A.chain_lds * 4 * kAddWavesPerBlock > 160 * 1024) return HM_ERR_UNSUPPORTED;
-    // MFMA chain (adder_mfma.hip): P_i within 2*kMfmaChunks-1 words and ab_i within 64 words (two
-    // tiles); carry bits for every tile plus the 64-word window overhang of the ring fill
+    // MFMA chain (adder_mfma.hip): P_i within 2*kMfmaChunks-1 words, ab_i within 64 words (two
+    // tiles), a bit's workspace record (x, P, ab, two degrees) within one 64-lane LDS-DMA; carry
+    // bits for every tile plus the 64-word window overhang of the ring fill
     {
         const uint32_t tiles = (SC + 31) / 32;
         const uint32_t mf_cw = 32 * tiles + 64;
         const uint32_t mf_lds = kMfmaHalo + mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
         const bool fits = maxPw <= 2 * kMfmaChunks - 1 && cntAB <= 64 &&
+                          cntX + cntP + cntAB + 2 <= 64 &&
                           (256 + (size_t)mf_lds * kAddWavesPerBlock) * 4 <= 160 * 1024;
         A.mfma = fits && c->add_chain != HM_ADD_CHAIN_VALU;
         if (c->add_chain == HM_ADD_CHAIN_MFMA && !fits) return HM_ERR_UNSUPPORTED;
@@ -666,7 +696,16 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     A.n = a->n, A.nbits = L;
     A.status = c->d_status;
     fill_bounds(A.ab, a), fill_bounds(A.bb, b), fill_bounds(A.ob, out);
-    return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+    void *ev[2] = {nullptr, nullptr};
+    if (c->time_chain) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(c->stream, &cap);
+        if (cap == hipStreamCaptureStatusNone && c->tev_used + 2 <= c->tev.size()) {
+            ev[0] = c->tev[c->tev_used], ev[1] = c->tev[c->tev_used + 1];
+            c->tev_used += 2;
+        }
+    }
+    return launch_add(A, c->stream, ev[0], ev[1]) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 
 hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,

@@ -66,6 +66,11 @@ struct hm_ctx {
     uint32_t ka_min = 1024, ka_leaf = 256;
     // carry chain of the adder (hm_ctx_set_add_options): HM_ADD_CHAIN_AUTO / _MFMA / _VALU
     uint32_t add_chain = 0;
+    // per-launch timing of the adder's carry-chain kernel (hm_ctx_set_kernel_timing): a pair of
+    // HIP events recorded around each chain launch on the engine stream
+    bool time_chain = false;
+    std::vector<hipEvent_t> tev; // 2 per recorded launch
+    size_t tev_used = 0;
 };
 
 namespace hm {

@@ -220,8 +220,10 @@ struct RandArgs {
 
 // host-side launchers (kernels.hip)
 int launch_random(const RandArgs &a, void *stream);
-int launch_add(const AddArgs &a, void *stream);
+// ev0/ev1 (hipEvent_t, may be null): recorded on the stream around the carry-chain launch
+int launch_add(const AddArgs &a, void *stream, void *ev0 = nullptr, void *ev1 = nullptr);
 int launch_add_chain_mfma(const AddArgs &a, void *stream);
+int launch_add_chain_valu(const AddArgs &a, void *stream);
 int launch_encrypt(const EncArgs &a, void *stream);
 int launch_decrypt(const DecArgs &a, void *stream);
 int launch_gate(const GateArgs &a, void *stream);
@@ -240,6 +242,7 @@ int launch_poly_mul(const PolyArgs &a, void *stream);
 int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
+constexpr size_t kTimedLaunches = 4096; // chain launches hm_ctx_set_kernel_timing can record
 // MFMA carry chain (adder_mfma.hip): P_i within 2*kMfmaChunks-1 words, nibble ring slots (a power
 // of two above the 58-word window of a tile plus the 32 words filled ahead), zero words below C
 constexpr int kMfmaChunks = 13;

@@ -438,6 +438,19 @@ class Context:
         _check(lib().hm_ctx_set_add_options(self._h, self.ADD_CHAINS[chain]),
                "hm_ctx_set_add_options")
 
+    def set_kernel_timing(self, enable: bool = True):
+        """hm_ctx_set_kernel_timing: record HIP events around every carry-chain launch of the
+        adder (outside graph capture) from now on; kernel_timing() reads them back."""
+        _check(lib().hm_ctx_set_kernel_timing(self._h, int(bool(enable))), "hm_ctx_set_kernel_timing")
+
+    def kernel_timing(self):
+        """(summed carry-chain kernel ms, launches) since set_kernel_timing(True)."""
+        t = ctypes.c_double(0.0)
+        n = ctypes.c_uint32(0)
+        _check(lib().hm_ctx_kernel_timing(self._h, ctypes.byref(t), ctypes.byref(n)),
+               "hm_ctx_kernel_timing")
+        return t.value, n.value
+
     def set_mul_options(self, karatsuba_min_words: int = 1024, karatsuba_leaf_words: int = 256):
         """hm_ctx_set_mul_options: which carry products of the multiplier run as Karatsuba
         recursions (shorter operand >= karatsuba_min_words words; 0 = never) and their leaf

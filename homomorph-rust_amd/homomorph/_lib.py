@@ -72,6 +72,8 @@ SIGNATURES = {
     "hm_validate_operation": (ctypes.c_int, [vp, ctypes.c_int, u16p]),
     "hm_ctx_set_mul_options": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
     "hm_ctx_set_add_options": (ctypes.c_int, [vp, ctypes.c_uint32]),
+    "hm_ctx_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+    "hm_ctx_kernel_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u32p]),
     "hm_fresh_bound": (ctypes.c_uint32, [vp]),
     "hm_add_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, u32p]),
     "hm_mul_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, ctypes.c_int, u32p]),

@@ -166,6 +166,14 @@ hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
 #define HM_ADD_CHAIN_VALU 2u
 hm_status hm_ctx_set_add_options(hm_ctx *ctx, uint32_t chain);
 
+/* Kernel timing (measurement only; no effect on results).  While enabled, every hm_add_batch
+ * outside a stream capture records a pair of HIP events on the engine stream around its
+ * carry-chain kernel (the dominant kernel of the add), up to 4096 launches; enabling resets the
+ * record.  hm_ctx_kernel_timing synchronizes the stream and returns the summed chain time and the
+ * number of launches recorded. */
+hm_status hm_ctx_set_kernel_timing(hm_ctx *ctx, int enable);
+hm_status hm_ctx_kernel_timing(hm_ctx *ctx, double *total_ms, uint32_t *launches);
+
 /* Context::validate_operation (src/context.rs:310-323): HM_OK or HM_ERR_INVALID_PARAMETERS with
  * the OperationError payload written to *required_min_d_over_delta (may be NULL). */
 hm_status hm_validate_operation(const hm_ctx *ctx, hm_op op, uint16_t *required_min_d_over_delta);

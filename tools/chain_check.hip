@@ -4,6 +4,7 @@
 // Modes: random words, or single set bits (localises index errors).  Prints the first mismatching
 // output words.  build: hipcc --offload-arch=gfx950 -O3 -I homomorph-rust_amd/csrc \
 //   tools/chain_check.hip -o tools/chain_check
+#define HM_MFMA_PROFILE 1
 #include "../homomorph-rust_amd/csrc/adder_mfma.hip"
 
 #include <cstdio>
@@ -30,7 +31,10 @@ static int degp1(const uint32_t *w, int n) {
 
 static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool quiet);
 
+static int timing(int nvals);
+
 int main(int argc, char **argv) {
+    if (argc > 1 && !strcmp(argv[1], "time")) return timing(argc > 2 ? atoi(argv[2]) : 4096);
     if (argc > 1 && !strcmp(argv[1], "sweep")) {
         const int ps[] = {0, 5, 31, 32, 100, 400, 650, 700, 736, 767};
         const int cs[] = {0, 7, 31, 32, 100, 300, 480, 511};
@@ -112,6 +116,11 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     hipMemset(dout, 0, A.out.stride * 8);
     hipMemset(dst, 0, 4);
     A.ws = dws, A.out.limbs = dout, A.out.degree = ddeg, A.status = dst;
+    static unsigned long long *dprof1 = nullptr;
+    if (!dprof1) {
+        hipMalloc(&dprof1, 64);
+        hipMemcpyToSymbol(HIP_SYMBOL(g_mfma_prof), &dprof1, sizeof dprof1);
+    }
     if (launch_add_chain_mfma(A, nullptr)) { printf("launch failed\n"); return 2; }
     hipDeviceSynchronize();
     std::vector<uint64_t> out(A.out.stride);
@@ -135,4 +144,68 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
                abw, mode, pbit, cbit, bad, st);
     hipFree(dws), hipFree(dout), hipFree(ddeg), hipFree(dst);
     return bad;
+}
+
+// configs[1]-shaped chain (32 bits, P 25 words, ab 17 words, x 9 words) replicated over nvals
+// values: kernel time and per-phase s_memtime sums (cycles summed over waves)
+static int timing(int nvals) {
+    const int L = 32;
+    const uint32_t cntAB = 17, cntP = 25, cntX = 9;
+    std::mt19937_64 rng(11);
+    AddArgs A{};
+    A.n = (uint64_t)nvals, A.nbits = L, A.cntAB = cntAB, A.cntP = cntP, A.cntX = cntX;
+    A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
+    std::vector<uint32_t> ws(A.ws_stride * nvals, 0u);
+    for (int v = 0; v < nvals; ++v) {
+        uint32_t *w = &ws[(size_t)v * A.ws_stride];
+        for (int i = 0; i < L; ++i) {
+            for (uint32_t k = 0; k < cntAB; ++k) w[i * cntAB + k] = (uint32_t)rng();
+            w[i * cntAB + cntAB - 1] &= 0x7FFFFFFFu;
+            for (uint32_t k = 0; k < cntP; ++k) w[L * cntAB + i * cntP + k] = k + 1 < cntP ? (uint32_t)rng() : 1u;
+            w[L * (cntAB + cntP) + i] = degp1(&w[i * cntAB], cntAB);
+            w[L * (cntAB + cntP) + L + i] = degp1(&w[L * cntAB + i * cntP], cntP);
+            for (uint32_t k = 0; k < cntX; ++k) w[L * (cntAB + cntP + 2) + i * cntX + k] = (uint32_t)rng() & (k + 1 < cntX ? ~0u : 1u);
+        }
+    }
+    const uint32_t maxw = 25 * L + 40;
+    const uint32_t outcap = (maxw * 32 + 63) / 64 + 1;
+    for (int i = 0; i < L; ++i) A.ob.b[i] = outcap * 64 - 1;
+    A.out.stride = (uint64_t)outcap * L;
+    const uint32_t tiles = (maxw + 31) / 32;
+    A.mf_cw = 32 * tiles + 64;
+    A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
+    A.mfma = 1;
+    uint32_t *dws, *ddeg;
+    uint64_t *dout;
+    int *dst;
+    hipMalloc(&dws, ws.size() * 4);
+    hipMalloc(&dout, A.out.stride * 8 * nvals);
+    hipMalloc(&ddeg, (size_t)L * 4 * nvals);
+    hipMalloc(&dst, 4);
+    hipMemcpy(dws, ws.data(), ws.size() * 4, hipMemcpyHostToDevice);
+    hipMemset(dst, 0, 4);
+    A.ws = dws, A.out.limbs = dout, A.out.degree = ddeg, A.status = dst;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0), hipEventCreate(&e1);
+    unsigned long long *dprof;
+    hipMalloc(&dprof, (size_t)nvals * 4 * 8);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_mfma_prof), &dprof, sizeof dprof);
+    launch_add_chain_mfma(A, nullptr);
+    hipDeviceSynchronize();
+    const int reps = 5;
+    hipEventRecord(e0);
+    for (int r = 0; r < reps; ++r) launch_add_chain_mfma(A, nullptr);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    std::vector<unsigned long long> hp((size_t)nvals * 4);
+    hipMemcpy(hp.data(), dprof, hp.size() * 8, hipMemcpyDeviceToHost);
+    double z[3] = {0, 0, 0};
+    for (int v = 0; v < nvals; ++v)
+        for (int k = 0; k < 3; ++k) z[k] += (double)hp[(size_t)v * 4 + k];
+    const double waves = (double)nvals; // the last launch's per-wave sums
+    printf("chain %d values: %.1f us per launch; per wave (s_memtime ticks): sum-store %.0f, RS+A build %.0f, tiles %.0f\n",
+           nvals, ms * 1e3 / reps, z[0] / waves, z[1] / waves, z[2] / waves);
+    return 0;
 }
