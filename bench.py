@@ -612,7 +612,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=["add", "mixed", "distcheck"], default="add",
                     help="add: configs[1] (headline); mixed: configs[4]; distcheck: CPU plumbing")
     ap.add_argument("--batch", type=int, default=0,

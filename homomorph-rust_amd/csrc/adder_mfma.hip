@@ -68,7 +68,11 @@ __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f 
 // them; an empty asm after each MFMA that names acc (so the MFMA stays above it: no instruction,
 // no wait) and clobbers memory (so later reads stay below it) pins the interleaving.
 constexpr int kPrefetch = 3;
-__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const uint4 *rb, v16f acc) {
+// side(k) runs after MFMA k for k = 1, 4, 7 (the next tile's ring fill in three stages: its LDS
+// latency hides under this tile's MFMAs instead of stalling the wave between tiles)
+template <class Side>
+__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const uint4 *rb, v16f acc,
+                                          Side &&side) {
     uint4 bq[kMfmaChunks];
 #pragma unroll
     for (int c = 0; c < kPrefetch; ++c) bq[c] = rb[2 * c];
@@ -78,6 +82,9 @@ __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const ui
         const v8i Bf = {(int)bq[c].x, (int)bq[c].y, (int)bq[c].z, (int)bq[c].w, 0, 0, 0, 0};
         acc = mfma_fp4(Af[c], Bf, acc);
         asm volatile("" : "+v"(acc)::"memory");
+        if (c == 1) side(0);
+        if (c == 4) side(1);
+        if (c == 7) side(2);
     }
     return acc;
 }
@@ -232,19 +239,42 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             wsync(); // ring images of this tile's window are written
             // window words 32T + col - D + h + 2c: one base slot, chunk c at +2c slots (32 B)
             const uint4 *rb = (const uint4 *)&ring[((32 * T + col - D + h) & (kMfmaRingSlots - 1)) * 4];
-            acc = tile_mfma(Af, rb, acc);
-            // the next tile's new window words (still the old carry: they lie below 32T)
-            if (T > 0) ring_fill(C, ring, tab, 32 * (T - 1) - D, 32);
-            // rows (j&3) + 8(j>>2) + 4h of column col: gather bit 0 of each accumulator
-            uint32_t g = 0u;
+            // the next tile's 32 new window words (old carry: below 32T; their ring slots are not
+            // in this tile's window), one per lane pair, staged between this tile's MFMAs
+            const int fw = 32 * (T - 1) - D + col;
+            uint32_t fv = 0u;
+            uint2 fn = {0u, 0u};
+            acc = tile_mfma(Af, rb, acc, [&](int stage) {
+                if (T == 0) return;
+                // (the empty asm keep each stage's arithmetic from being hoisted into an earlier
+                // stage, where it would wait for the read of the stage before)
+                if (stage == 0) fv = C[fw];
+                else if (stage == 1) {
+                    asm volatile("" : "+v"(fv));
+                    fv >>= 16 * h;
+                    fn.x = tab[fv & 0xFFu], fn.y = tab[(fv >> 8) & 0xFFu];
+                } else {
+                    asm volatile("" : "+v"(fn.x), "+v"(fn.y));
+                    uint32_t *slot = &ring[(fw & (kMfmaRingSlots - 1)) * 4 + 2 * h];
+                    *(uint2 *)slot = fn;
+                    *(uint2 *)(slot + 4 * kMfmaRingSlots) = fn;
+                }
+            });
+            // rows (j&3) + 8(j>>2) + 4h of column col: gather bit 0 of each accumulator, four
+            // independent 4-deep chains (nibble q = accumulators 4q .. 4q+3)
+            uint32_t nq[4];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) g = funnel(__float_as_uint(acc[j]), g, 1);
-            g >>= 16;
-            const uint32_t gnow = g;
-            g ^= gprev; // bit j = row (j&3) + 8(j>>2) + 4h
-            gprev = gnow;
-            uint32_t t = (g | (g << 8)) & 0x00FF00FFu;
-            t = ((t | (t << 4)) & 0x0F0F0F0Fu) << (4 * h);
+            for (int q = 0; q < 4; ++q) {
+                uint32_t x = 0u;
+#pragma unroll
+                for (int j = 4 * q; j < 4 * q + 4; ++j) x = funnel(__float_as_uint(acc[j]), x, 1);
+                nq[q] = x >> 28; // bit j-4q = accumulator j
+            }
+            // nibble q to bits 8q .. 8q+3 (rows 8q + 4h + i sit at bit 8q + 4h + i), XOR the bits
+            // of the accumulators before this tile
+            const uint32_t tnow = nq[0] | (nq[1] << 8) | (nq[2] << 16) | (nq[3] << 24);
+            const uint32_t t = (tnow ^ gprev) << (4 * h);
+            gprev = tnow;
             const uint32_t word = t | (uint32_t)__shfl_xor((int)t, 32, 64);
             const int W = 32 * T + col;
             const uint32_t v = word ^ (W < nab ? abi[W] : 0u); // ab_i < 64 words (host plan)

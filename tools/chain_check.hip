@@ -168,9 +168,13 @@ static int timing(int nvals) {
         }
     }
     const uint32_t maxw = 25 * L + 40;
-    const uint32_t outcap = (maxw * 32 + 63) / 64 + 1;
-    for (int i = 0; i < L; ++i) A.ob.b[i] = outcap * 64 - 1;
-    A.out.stride = (uint64_t)outcap * L;
+    // the add's output bounds at d + d' = 256 (hm_add_out_bounds): s_0 <= 256, s_i <= (3i-1)*256
+    uint64_t stride = 0;
+    for (int i = 0; i < L; ++i) {
+        A.ob.b[i] = i == 0 ? 256u : (uint32_t)(3 * i - 1) * 256u;
+        stride += A.ob.b[i] / 64 + 1;
+    }
+    A.out.stride = stride;
     const uint32_t tiles = (maxw + 31) / 32;
     A.mf_cw = 32 * tiles + 64;
     A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
