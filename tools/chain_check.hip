@@ -66,6 +66,7 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
         if (mode == 0) {
             for (auto &w : P[i]) w = (uint32_t)rng();
             for (auto &w : AB[i]) w = (uint32_t)rng();
+            for (auto &w : X[i]) w = (uint32_t)rng();
         } else {
             P[i][pbit / 32] = 1u << (pbit % 32);
             if (i == 0) AB[i][cbit / 32] = 1u << (cbit % 32);
@@ -113,7 +114,7 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     hipMalloc(&ddeg, L * 4);
     hipMalloc(&dst, 4);
     hipMemcpy(dws, ws.data(), ws.size() * 4, hipMemcpyHostToDevice);
-    hipMemset(dout, 0, A.out.stride * 8);
+    hipMemset(dout, 0xA5, A.out.stride * 8); // every output word must be written
     hipMemset(dst, 0, 4);
     A.ws = dws, A.out.limbs = dout, A.out.degree = ddeg, A.status = dst;
     static unsigned long long *dprof1 = nullptr;
@@ -127,8 +128,16 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     hipMemcpy(out.data(), dout, out.size() * 8, hipMemcpyDeviceToHost);
     int st;
     hipMemcpy(&st, dst, 4, hipMemcpyDeviceToHost);
+    std::vector<uint32_t> gdeg(L);
+    hipMemcpy(gdeg.data(), ddeg, L * 4, hipMemcpyDeviceToHost);
     int bad = 0;
     for (int i = 0; i < L; ++i) {
+        const int dp1 = degp1(S[i].data(), (int)S[i].size());
+        const uint32_t want = dp1 ? (uint32_t)(dp1 - 1) : 0u;
+        if (gdeg[i] != want) {
+            ++bad;
+            if (!quiet) printf("bit %d degree: gpu %u ref %u\n", i, gdeg[i], want);
+        }
         const uint32_t *g = (const uint32_t *)&out[(size_t)i * outcap];
         int shown = 0;
         for (size_t k = 0; k < 2 * outcap; ++k) {
