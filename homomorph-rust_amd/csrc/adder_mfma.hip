@@ -57,6 +57,15 @@ __device__ unsigned long long *g_mfma_prof; // 4 per wave, set by the harness
 #define HM_PACC(k, a, b)
 #endif
 
+// The lane index as an opaque value: lane-derived addresses computed from it inside the bit loop
+// stay there (hoisted out of it they were live across the whole chain and spilled to scratch,
+// whose reloads then waited on every outstanding global access of the bit)
+__device__ __forceinline__ int lane_opaque() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
     // cbsz = blgp = 4: both operands fp4 e2m1; E8M0 scales 127 = 1.0
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
@@ -71,14 +80,18 @@ constexpr int kPrefetch = 3;
 // side(k) runs after MFMA k for k = 1, 4, 7 (the next tile's ring fill in three stages: its LDS
 // latency hides under this tile's MFMAs instead of stalling the wave between tiles)
 template <class Side>
-__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const uint4 *rb, v16f acc,
-                                          Side &&side) {
+__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const uint4 *rb, const uint4 *rbn,
+                                          uint4 (&pf)[kPrefetch], v16f acc, Side &&side) {
+    // pf holds this tile's first kPrefetch B fragments (read during the tile before); the last
+    // kPrefetch reads of this tile fetch the next tile's (window base rbn; its ring fill is side
+    // stage 2, issued above them), so the next tile's first MFMA does not wait for the LDS
     uint4 bq[kMfmaChunks];
 #pragma unroll
-    for (int c = 0; c < kPrefetch; ++c) bq[c] = rb[2 * c];
+    for (int c = 0; c < kPrefetch; ++c) bq[c] = pf[c];
 #pragma unroll
     for (int c = 0; c < kMfmaChunks; ++c) {
         if (c + kPrefetch < kMfmaChunks) bq[c + kPrefetch] = rb[2 * (c + kPrefetch)];
+        else pf[c + kPrefetch - kMfmaChunks] = rbn[2 * (c + kPrefetch - kMfmaChunks)];
         const v8i Bf = {(int)bq[c].x, (int)bq[c].y, (int)bq[c].z, (int)bq[c].w, 0, 0, 0, 0};
         acc = mfma_fp4(Af[c], Bf, acc);
         asm volatile("" : "+v"(acc)::"memory");
@@ -94,8 +107,7 @@ __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const ui
 // slot is written twice, at s and s + kMfmaRingSlots, so a tile's window [slot, slot + 2*NC) is
 // contiguous wherever it starts: its B reads share one address and differ by immediates.
 __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, const uint32_t *tab,
-                                          int base, int count) {
-    const int lane = lane_id();
+                                          int base, int count, int lane) {
     const int h = lane >> 5;
     for (int k = lane & 31; k < count; k += 32) {
         const int w = base + k;
@@ -171,14 +183,36 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
     for (uint32_t k = lane; k < kMfmaHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
     for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u; // P below bit 0
     wsync();
-    int nc = 0; // carry words (0 = null carry, common.rs:39)
+    int nc = 0;    // carry words (0 = null carry, common.rs:39)
+    int degc = -1; // the carry's degree
+    int tw = -1;   // > 0: the previous bit's tiles stored sum words [cntX, min(tw, cap words))
     uint32_t offo = 0;
     for (uint32_t i = 0; i < L; ++i) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
         const uint32_t *rec = &stage[wave][i & 1][0];
         // s_i = x_i ^ carry_i (common.rs:43-47)
         HM_PT(t0);
-        store_sum_x(rec, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
+        if (tw < 0) {
+            store_sum_x(rec, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
+        } else {
+            // the tiles wrote s_i's words from cntX up (= carry words there); left: the words
+            // below cntX (x_i ^ carry), zeros above the tiles, the degree
+            const int capw = 2 * (int)cap_of(A.ob.b[i]);
+            uint32_t *so = (uint32_t *)(po + offo);
+            int ldeg = -1;
+            if (lane < (int)A.cntX) {
+                const uint32_t v = rec[lane] ^ C[lane]; // C is valid up to tw > cntX words
+                so[lane] = v;
+                if (v) ldeg = lane * 32 + 31 - (int)__builtin_clz(v);
+            }
+            for (int w = tw + lane; w < capw; w += kWave) so[w] = 0u;
+            int deg = wave_max_i32(ldeg);
+            if (nc > (int)A.cntX) deg = degc; // the carry's top word is above x_i
+            if (lane == 0) {
+                if (deg > (int)A.ob.b[i]) flag(A.status, HM_ERR_CAPACITY);
+                dout[i] = (uint32_t)max(deg, 0);
+            }
+        }
         offo += cap_of(A.ob.b[i]);
         HM_PT(t1);
         HM_PACC(0, t0, t1);
@@ -191,6 +225,7 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             const int n = max(nc, nab);
             for (int w = lane; w < n; w += kWave) C[w] = w < nab ? abi[w] : 0u;
             nc = nab;
+            tw = -1;
             wsync();
             stage_rec(i + 1);
             continue;
@@ -210,14 +245,18 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
         // P indices are negative), so the chunk loop has no branches and its reads can be issued
         // ahead of the MFMAs.
         const int D = np;
+        const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
         // A fragments: lane (row m = col, half h), chunk c holds P[s - e], s = 32(D-2c-h) + m,
         // i.e. RS nibbles j0 .. j0+31 with j0 = 32*kRevWords - 1 - s: five words, four funnels
+        // j0 of chunk c = jb + 64c (jb >= 64 since D <= 25 < kRevWords - 1): one base word per
+        // lane, chunk c at +8c words (immediate offsets), one shift for all chunks
         v8i Af[kMfmaChunks];
+        const int jb = 32 * (kRevWords - D + h) - 1 - col;
+        const uint32_t *rw0 = RS + (jb >> 3);
+        const uint32_t sh = 4u * (uint32_t)(jb & 7);
 #pragma unroll
         for (int c = 0; c < kMfmaChunks; ++c) {
-            const int j0 = 32 * kRevWords - 1 - (32 * (D - 2 * c - h) + col);
-            const uint32_t *rw = RS + (j0 >> 3);
-            const uint32_t sh = 4u * (uint32_t)(j0 & 7);
+            const uint32_t *rw = rw0 + 8 * c;
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3], w4 = rw[4];
             Af[c] = (v8i){(int)funnel(w1, w0, sh), (int)funnel(w2, w1, sh), (int)funnel(w3, w2, sh),
                           (int)funnel(w4, w3, sh), 0, 0, 0, 0};
@@ -226,7 +265,12 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
         HM_PACC(1, t1, t2);
         const int nout = max(nc + np, nab);
         const int tiles = (nout + 31) >> 5;
-        ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64);
+        // s_{i+1}'s words from cntX up are carry_{i+1}'s: the tiles store them (u32 words of the
+        // output limbs) below the output's capacity; bit i+1 does the rest
+        uint32_t *son = (uint32_t *)(po + offo);
+        const int capn = 2 * (int)cap_of(A.ob.b[i + 1]);
+        const int wlo = (int)A.cntX;
+        ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64, lane);
         int ldeg = -1;
         // The accumulators start at 2^23 once per bit and keep accumulating tile after tile
         // (2^23 + every count stays below 2^24, exact): a tile's parities are bit 0 of its
@@ -235,16 +279,26 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = 8388608.0f;
         uint32_t gprev = 0u;
+        // window words 32T + col - D + h + 2c: one base slot, chunk c at +2c slots (32 B)
+        auto rbase = [&](int T) {
+            return (const uint4 *)&ring[((32 * T + col - D + h) & (kMfmaRingSlots - 1)) * 4];
+        };
+        wsync(); // the first tile's ring images are written
+        uint4 pf[kPrefetch];
+#pragma unroll
+        for (int c = 0; c < kPrefetch; ++c) pf[c] = rbase(tiles - 1)[2 * c];
         for (int T = tiles - 1; T >= 0; --T) {
             wsync(); // ring images of this tile's window are written
-            // window words 32T + col - D + h + 2c: one base slot, chunk c at +2c slots (32 B)
-            const uint4 *rb = (const uint4 *)&ring[((32 * T + col - D + h) & (kMfmaRingSlots - 1)) * 4];
+            const uint4 *rb = rbase(T), *rbn = rbase(T - 1); // (T = 0: rbn reads are not used)
             // the next tile's 32 new window words (old carry: below 32T; their ring slots are not
             // in this tile's window), one per lane pair, staged between this tile's MFMAs
             const int fw = 32 * (T - 1) - D + col;
             uint32_t fv = 0u;
             uint2 fn = {0u, 0u};
-            acc = tile_mfma(Af, rb, acc, [&](int stage) {
+            // ab_i's word of this tile's output, read before the MFMAs (ab_i < 64 words: host plan)
+            const int W = 32 * T + col;
+            const uint32_t abw = W < nab ? abi[W] : 0u;
+            acc = tile_mfma(Af, rb, rbn, pf, acc, [&](int stage) {
                 if (T == 0) return;
                 // (the empty asm keep each stage's arithmetic from being hoisted into an earlier
                 // stage, where it would wait for the read of the stage before)
@@ -275,14 +329,20 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             const uint32_t tnow = nq[0] | (nq[1] << 8) | (nq[2] << 16) | (nq[3] << 24);
             const uint32_t t = (tnow ^ gprev) << (4 * h);
             gprev = tnow;
-            const uint32_t word = t | (uint32_t)__shfl_xor((int)t, 32, 64);
-            const int W = 32 * T + col;
-            const uint32_t v = word ^ (W < nab ? abi[W] : 0u); // ab_i < 64 words (host plan)
-            if (h == 0) C[W] = v;
+            // the two lane halves' bits meet by one v_permlane32_swap (VALU; no LDS round trip)
+            const auto sw = __builtin_amdgcn_permlane32_swap(t, t, false, false);
+            const uint32_t word = sw[0] | sw[1];
+            const uint32_t v = word ^ abw;
+            if (h == 0) {
+                C[W] = v;
+                if (W >= wlo && W < capn) son[W] = v;
+            }
             if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
         }
         const int deg = wave_max_i32(ldeg);
         nc = deg >= 0 ? (deg >> 5) + 1 : 0;
+        degc = deg;
+        tw = 32 * tiles;
         wsync();
         HM_PT(t3);
         HM_PACC(2, t2, t3);
