@@ -195,19 +195,20 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
         if (tw < 0) {
             store_sum_x(rec, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
         } else {
-            // the tiles wrote s_i's words from cntX up (= carry words there); left: the words
-            // below cntX (x_i ^ carry), zeros above the tiles, the degree
+            // the tiles T >= 1 wrote s_i's words from 32 up (= carry words there); left: words
+            // 0..31 (x_i ^ carry; stored here rather than by tile 0, whose stores would still be
+            // in flight at this bit's vmcnt wait), zeros above the tiles, the degree
             const int capw = 2 * (int)cap_of(A.ob.b[i]);
             uint32_t *so = (uint32_t *)(po + offo);
             int ldeg = -1;
-            if (lane < (int)A.cntX) {
-                const uint32_t v = rec[lane] ^ C[lane]; // C is valid up to tw > cntX words
+            if (lane < 32 && lane < capw) { // C is valid up to tw >= 32 words; cntX < 32
+                const uint32_t v = (lane < (int)A.cntX ? rec[lane] : 0u) ^ C[lane];
                 so[lane] = v;
                 if (v) ldeg = lane * 32 + 31 - (int)__builtin_clz(v);
             }
             for (int w = tw + lane; w < capw; w += kWave) so[w] = 0u;
             int deg = wave_max_i32(ldeg);
-            if (nc > (int)A.cntX) deg = degc; // the carry's top word is above x_i
+            if (nc > 32) deg = degc; // the carry's top word is above the words stored here
             if (lane == 0) {
                 if (deg > (int)A.ob.b[i]) flag(A.status, HM_ERR_CAPACITY);
                 dout[i] = (uint32_t)max(deg, 0);
@@ -265,11 +266,11 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
         HM_PACC(1, t1, t2);
         const int nout = max(nc + np, nab);
         const int tiles = (nout + 31) >> 5;
-        // s_{i+1}'s words from cntX up are carry_{i+1}'s: the tiles store them (u32 words of the
-        // output limbs) below the output's capacity; bit i+1 does the rest
+        // s_{i+1}'s words from 32 up are carry_{i+1}'s (x_{i+1} < 32 words): tiles T >= 1 store
+        // them (u32 words of the output limbs) below the output's capacity; bit i+1 does the rest
         uint32_t *son = (uint32_t *)(po + offo);
         const int capn = 2 * (int)cap_of(A.ob.b[i + 1]);
-        const int wlo = (int)A.cntX;
+        const int wlo = 32;
         ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64, lane);
         int ldeg = -1;
         // The accumulators start at 2^23 once per bit and keep accumulating tile after tile
@@ -298,6 +299,7 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
             // ab_i's word of this tile's output, read before the MFMAs (ab_i < 64 words: host plan)
             const int W = 32 * T + col;
             const uint32_t abw = W < nab ? abi[W] : 0u;
+            __builtin_amdgcn_s_setprio(1); // the MFMA phase keeps the pipe
             acc = tile_mfma(Af, rb, rbn, pf, acc, [&](int stage) {
                 if (T == 0) return;
                 // (the empty asm keep each stage's arithmetic from being hoisted into an earlier
@@ -314,6 +316,7 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
                     *(uint2 *)(slot + 4 * kMfmaRingSlots) = fn;
                 }
             });
+            __builtin_amdgcn_s_setprio(0);
             // rows (j&3) + 8(j>>2) + 4h of column col: gather bit 0 of each accumulator, four
             // independent 4-deep chains (nibble q = accumulators 4q .. 4q+3)
             uint32_t nq[4];
