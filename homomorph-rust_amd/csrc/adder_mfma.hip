@@ -76,7 +76,10 @@ __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f 
 // compiler hoists all 13 reads (13 x 4 VGPRs beside A's 52: spills) and sinks the MFMAs below
 // them; an empty asm after each MFMA that names acc (so the MFMA stays above it: no instruction,
 // no wait) and clobbers memory (so later reads stay below it) pins the interleaving.
-constexpr int kPrefetch = 3;
+#ifndef HM_MFMA_PREFETCH
+#define HM_MFMA_PREFETCH 3
+#endif
+constexpr int kPrefetch = HM_MFMA_PREFETCH;
 // side(k) runs after MFMA k for k = 1, 4, 7 (the next tile's ring fill in three stages: its LDS
 // latency hides under this tile's MFMAs instead of stalling the wave between tiles)
 template <class Side>
@@ -121,9 +124,18 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
     }
 }
 
-__global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
+// waves per block (<= kAddWavesPerBlock, which the host plan's LDS check assumes)
+#ifndef HM_MFMA_WPB
+#define HM_MFMA_WPB kAddWavesPerBlock
+#endif
+constexpr int kMfmaWpb = HM_MFMA_WPB;
+static_assert(kMfmaWpb <= kAddWavesPerBlock, "host LDS plan");
+
+// 4 waves per SIMD (the batch's 4096 waves fill the chip at that): 128 VGPRs
+__global__ void __launch_bounds__(64 * kMfmaWpb) __attribute__((amdgpu_waves_per_eu(4, 4)))
+add_chain_mfma_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
-    __shared__ uint32_t stage[kAddWavesPerBlock][2][64];
+    __shared__ uint32_t stage[kMfmaWpb][2][64];
     uint32_t *tab = lds; // byte -> 8 nibbles, fp4 1.0 (0b0010) per set bit
     for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
         uint32_t v = 0u;
@@ -357,7 +369,7 @@ __global__ void __launch_bounds__(256, 4) add_chain_mfma_kernel(AddArgs A) {
 }
 
 int launch_add_chain_mfma(const AddArgs &a, void *stream) {
-    const int wpb = kAddWavesPerBlock;
+    const int wpb = kMfmaWpb;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     const size_t lds = (256 + (size_t)a.chain_lds * wpb) * 4;
     hipLaunchKernelGGL(add_chain_mfma_kernel, dim3((unsigned)blocks), dim3(64 * wpb), lds,
