@@ -173,15 +173,24 @@ __device__ __forceinline__ void holey_acc(uint32_t z[4], const Holey &U, const H
                                           const Holey &V0) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        uint32_t lo = 0u, hi = 0u;
+        uint32_t lo[4], hi[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
             const int b = (c - a) & 3;
-            lo ^= U.h[a] * V1.h[b];
-            hi ^= __umulhi(U.h[a], V0.h[b]);
+            lo[a] = U.h[a] * V1.h[b];
+            hi[a] = __umulhi(U.h[a], V0.h[b]);
         }
-        z[c] ^= lo ^ hi;
+        // nine-term XOR as four three-input v_bitop3
+        z[c] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(z[c], lo[0], lo[1], 0x96),
+                                           __builtin_amdgcn_bitop3_b32(lo[2], lo[3], hi[0], 0x96),
+                                           __builtin_amdgcn_bitop3_b32(hi[1], hi[2], hi[3], 0x96), 0x96);
     }
+}
+
+// a ^ b ^ c ^ d as one three-input v_bitop3 (truth table 0x96) and one XOR (the compiler does not
+// form bitop3 from XOR chains on its own)
+__device__ __forceinline__ uint32_t xor4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96) ^ d;
 }
 
 __device__ __forceinline__ uint32_t holey_fold(const uint32_t z[4]) {
@@ -213,18 +222,24 @@ __device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__rest
                                               uint32_t *out) {
     const Holey U(u);
     uint32_t hiprev = 0u;
+    // pv[k] is read one step ahead (the LDS latency hides under the step before), and each
+    // residue class XORs its four products as one expression (v_bitop3 three-input XORs)
+    uint32_t vnext = nv > 0 ? pv[0] : 0u;
     for (int k = 0; k <= nv; ++k) {
         uint32_t lo = 0u, hi = 0u;
         if (k < nv) {
-            const Holey V(pv[k]);
-            uint64_t z[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) z[(a + b) & 3] ^= (uint64_t)U.h[a] * V.h[b];
+            const Holey V(vnext);
+            vnext = k + 1 < nv ? pv[k + 1] : 0u;
             uint32_t zl[4], zh[4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) zl[c] = (uint32_t)z[c], zh[c] = (uint32_t)(z[c] >> 32);
+            for (int c = 0; c < 4; ++c) {
+                uint64_t p[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) p[a] = (uint64_t)U.h[a] * V.h[(c - a) & 3];
+                zl[c] = xor4((uint32_t)p[0], (uint32_t)p[1], (uint32_t)p[2], (uint32_t)p[3]);
+                zh[c] = xor4((uint32_t)(p[0] >> 32), (uint32_t)(p[1] >> 32), (uint32_t)(p[2] >> 32),
+                             (uint32_t)(p[3] >> 32));
+            }
             lo = holey_fold(zl), hi = holey_fold(zh);
         }
         const uint32_t w = lo ^ hiprev;
