@@ -476,12 +476,15 @@ def run_add(args, world, rank, device):
     chain_s = chain_ms / 1e3 / max(1, chain_n)
     pairs = chain_bit_pairs(ca.bound, cb.bound)
     achieved = 2.0 * pairs * n / chain_s / 1e12  # TFLOP/s: one bit-pair AND+XOR = one MAC = 2 ops
-    traffic = None
+    traffic, issue = None, {}
     try:
         with open(args.traffic) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch_per_4096")
+            tj = json.load(f)
+        traffic = tj.get("hbm_bytes_per_launch_per_4096")
         if traffic is not None:
             traffic = traffic * n / 4096
+        ck = tj.get("kernels", {}).get("hm::add_chain_mfma_kernel", {})
+        issue = {key: ck[key] for key in ("mfma_busy_frac", "valu_active_frac") if key in ck}
     except (OSError, ValueError):
         traffic = None
 
@@ -508,6 +511,9 @@ def run_add(args, world, rank, device):
                                "fp4 MFMA)",
                      "kernel_ms": 1e3 * chain_s, "kernel_ms_source": chain_src,
                      "alg_bit_pairs_per_add": pairs, "step_kernels_ms": 1e3 * kernel_s,
+                     # PMC issue shares of the chain kernel (profiles/add_traffic.json, same passes
+                     # as traffic): matrix-core busy cycles and VALU-active cycles over SIMD-cycles
+                     **issue,
                      "hbm_gbs_step": n * per_add / kernel_s / 1e9, "alg_bytes_per_add": per_add,
                      "note": "algorithmic work = schoolbook bit pairs of the chain's carry products "
                              "P_i * carry_i over the static degree bounds (DESIGN.md s4.1); "

@@ -17,7 +17,9 @@ per = {}
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
-        if "add_" not in k or r["Counter_Name"] not in ("FETCH_SIZE", "WRITE_SIZE"):
+        if "add_" not in k or r["Counter_Name"] not in (
+                "FETCH_SIZE", "WRITE_SIZE", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES",
+                "SQ_ACTIVE_INST_VALU"):
             continue
         per.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 kern = {}
@@ -27,6 +29,16 @@ for k, d in per.items():
     write = 1024 * sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
     kern[k] = {"fetch_bytes_x2": fetch, "write_bytes": write}
     total += fetch + write
+    # issue shares over the dispatch: SIMD-cycles = 1024 SIMDs x GRBM_GUI_ACTIVE / 8 (summed over
+    # the 8 XCDs); MFMA busy counts cycles, SQ_ACTIVE_INST_VALU quad-cycles summed over waves
+    if "GRBM_GUI_ACTIVE" in d:
+        simd_cyc = 1024 * (sum(d["GRBM_GUI_ACTIVE"]) / len(d["GRBM_GUI_ACTIVE"])) / 8
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in d:
+            kern[k]["mfma_busy_frac"] = sum(d["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(
+                d["SQ_VALU_MFMA_BUSY_CYCLES"]) / simd_cyc
+        if "SQ_ACTIVE_INST_VALU" in d:
+            kern[k]["valu_active_frac"] = 4 * sum(d["SQ_ACTIVE_INST_VALU"]) / len(
+                d["SQ_ACTIVE_INST_VALU"]) / simd_cyc
 res = {"hbm_bytes_per_launch_per_4096": total * 4096 / batch, "batch": batch, "kernels": kern,
        "source": root, "method": "2*FETCH_SIZE + WRITE_SIZE (KiB) per dispatch, rocprofv3 --pmc, "
                                  "separate passes; MI355X_MICROARCH.md HBM section"}
