@@ -213,9 +213,10 @@ add_chain_mfma_kernel(AddArgs A) {
             const int capw = 2 * (int)cap_of(A.ob.b[i]);
             uint32_t *so = (uint32_t *)(po + offo);
             int ldeg = -1;
-            if (lane < 32 && lane < capw) { // C is valid up to tw >= 32 words; cntX < 32
+            if (lane < 32) { // C is valid up to tw >= 32 words; cntX < 32
                 const uint32_t v = (lane < (int)A.cntX ? rec[lane] : 0u) ^ C[lane];
-                so[lane] = v;
+                if (lane < capw) so[lane] = v;
+                // (a word past the capacity still counts: the degree check below flags it)
                 if (v) ldeg = lane * 32 + 31 - (int)__builtin_clz(v);
             }
             for (int w = tw + lane; w < capw; w += kWave) so[w] = 0u;

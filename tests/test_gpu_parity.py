@@ -416,3 +416,23 @@ def test_mul_karatsuba_low16_matches_schoolbook(H):
     kl, kd = ka.to_host()
     sl, sd = sb.to_host()
     assert_batches_equal(kl, kd, sl, sd, ka.bound, 3, "K=16 karatsuba vs schoolbook")
+
+
+@pytest.mark.parametrize("chain", ["mfma", "valu"])
+def test_add_output_capacity_is_checked(H, chain):
+    """An add into outputs whose static bounds are below the circuit's (sum bits of degree up to
+    (3i-1)D) never truncates silently: the engine refuses the batch or flags HM_ERR_CAPACITY, on
+    both carry chains (the MFMA chain stores sum words from its tiles and checks the degree once
+    per bit)."""
+    params = (64, 64, 1, 64)
+    ctx = make_ctx(H, params, 41)
+    ctx.set_add_options(chain)
+    n = 4
+    a, b = plain(n, np.uint8, 42), plain(n, np.uint8, 43)
+    ca = ctx.encrypt(a, masks=masks(n, 8, 64, 44))
+    cb = ctx.encrypt(b, masks=masks(n, 8, 64, 45))
+    small = np.minimum(H.add_out_bounds(ca.bound, cb.bound), 200).astype(np.uint32)
+    out = H.Ciphered.empty(n, small, ca.limbs.device, np.dtype(np.uint8))
+    with pytest.raises(H.EngineError):
+        H.add_into(ctx, ca, cb, out)
+        ctx.synchronize()
