@@ -530,43 +530,64 @@ def run_add(args, world, rank, device):
     return result
 
 
+class MixedWorkload:
+    """configs[4]'s per-rank state: keys (rank 0's, broadcast), this rank's shard of the global
+    batch encrypted, the output batches, and the launch chunks.  `step()` is one pass of the
+    workload: per chunk of MIXED_CHUNK values one u32 add and one u32 multiply reduced to its low
+    MUL_LOW_K result bits.  Shared by run_mixed, the default bench's `secondary` line and the
+    full-batch test (tests/test_gpu_properties.py)."""
+
+    def __init__(self, world, rank, device, glob):
+        if glob % world:
+            raise SystemExit("--batch must divide by the number of ranks")
+        self.world, self.rank, self.glob = world, rank, glob
+        self.ctx = ctx = make_context(world, rank, device, MIXED_PARAMS)
+        self.n = n = glob // world
+        self.a, self.b = shard_inputs(rank, n)
+        self.ca, self.cb = ctx.encrypt(self.a), ctx.encrypt(self.b)  # seeded engine CSPRNG masks
+        self.sums = H.Ciphered.empty(n, H.add_out_bounds(self.ca.bound, self.cb.bound),
+                                     ctx.device, np.dtype(np.uint32))
+        kb = H.mul_out_bounds(self.ca.bound[:MUL_LOW_K], self.cb.bound[:MUL_LOW_K])
+        self.prods = H.Ciphered.empty(n, kb, ctx.device, np.dtype(np.uint8))
+        self.chunks = [(lo, min(n, lo + MIXED_CHUNK)) for lo in range(0, n, MIXED_CHUNK)]
+        self.views = [tuple(H.value_slice(c, lo, hi) for c in (self.ca, self.cb, self.sums,
+                                                                  self.prods))
+                      for lo, hi in self.chunks]
+        ctx.synchronize()
+
+    def step(self):
+        for va, vb, vs, vp in self.views:
+            H.add_into(self.ctx, va, vb, vs)
+            H.mul_low_into(self.ctx, va, vb, MUL_LOW_K, vp)
+
+    def verify(self, device, wall):
+        """Decrypt on device, gather every rank's plaintexts (RCCL all_gather), count the
+        correct sums and products on every rank; returns (ok_sums, ok_products, max wall)."""
+        ctx, n, world = self.ctx, self.n, self.world
+        res = torch.cat([ctx.decrypt_bytes(self.sums), ctx.decrypt_bytes(self.prods)], dim=1)
+        got, wall = gather_results(world, device, res, wall)
+        want_s, want_p = [], []
+        for r in range(world):
+            ra, rb = shard_inputs(r, n)
+            want_s.append((ra + rb).astype(np.uint32))
+            want_p.append((ra.astype(np.uint64) * rb % (1 << MUL_LOW_K)).astype(np.uint8))
+        ok_s = int(np.sum(np.ascontiguousarray(got[:, :4]).view("<u4").reshape(-1) ==
+                          np.concatenate(want_s)))
+        ok_p = int(np.sum(got[:, 4] == np.concatenate(want_p)))
+        return ok_s, ok_p, wall
+
+
 def run_mixed(args, world, rank, device):
     """configs[4]: u32 mixed add + mul at d = dp = tau = 256, global batch 2^20 sharded over the
     ranks (strong scaling), RCCL gather of the decrypted results.  Per value: one u32 add and one
     u32 multiply reduced to its low MUL_LOW_K result bits (the full u32 multiply circuit is
     infeasible; its low bits are bit-exact, row A14).  Each rank processes its
     shard in launches of MIXED_CHUNK values."""
-    ctx = make_context(world, rank, device, MIXED_PARAMS)
     glob = args.batch or (1 << 20)
-    if glob % world:
-        raise SystemExit("--batch must divide by the number of ranks")
-    n = glob // world
-    a, b = shard_inputs(rank, n)
-    ca, cb = ctx.encrypt(a), ctx.encrypt(b)  # masks from the (seeded) engine CSPRNG
-    sums = H.Ciphered.empty(n, H.add_out_bounds(ca.bound, cb.bound), device, np.dtype(np.uint32))
-    kb = H.mul_out_bounds(ca.bound[:MUL_LOW_K], cb.bound[:MUL_LOW_K])
-    prods = H.Ciphered.empty(n, kb, device, np.dtype(np.uint8))
-    chunks = [(lo, min(n, lo + MIXED_CHUNK)) for lo in range(0, n, MIXED_CHUNK)]
-    views = [tuple(H.value_slice(c, lo, hi) for c in (ca, cb, sums, prods)) for lo, hi in chunks]
-    ctx.synchronize()
-
-    def step():
-        for va, vb, vs, vp in views:
-            H.add_into(ctx, va, vb, vs)
-            H.mul_low_into(ctx, va, vb, MUL_LOW_K, vp)
-
-    wall, ev_s = time_loop(step, args.steps, args.warmup, world, ctx.stream)
-    ctx.synchronize()
-    res = torch.cat([ctx.decrypt_bytes(sums), ctx.decrypt_bytes(prods)], dim=1)  # n x 5 bytes
-    got, wall = gather_results(world, device, res, wall)
-    want_s, want_p = [], []
-    for r in range(world):
-        ra, rb = shard_inputs(r, n)
-        want_s.append((ra + rb).astype(np.uint32))
-        want_p.append((ra.astype(np.uint64) * rb % (1 << MUL_LOW_K)).astype(np.uint8))
-    ok_s = int(np.sum(np.ascontiguousarray(got[:, :4]).view("<u4").reshape(-1) ==
-                      np.concatenate(want_s)))
-    ok_p = int(np.sum(got[:, 4] == np.concatenate(want_p)))
+    w = MixedWorkload(world, rank, device, glob)
+    wall, ev_s = time_loop(w.step, args.steps, args.warmup, world, w.ctx.stream)
+    w.ctx.synchronize()
+    ok_s, ok_p, wall = w.verify(device, wall)
     total = glob * args.steps
     return {
         "metric": "homomorphic u32 ops/sec (add, mul) at d=dp=tau=256; 1/2/4/8 MI355X",
@@ -582,7 +603,7 @@ def run_mixed(args, world, rank, device):
         "dtype": "u32",
         "data": "synthetic: seeded u32 plaintexts, seeded keys, subset masks from the seeded engine CSPRNG",
         "config": {"workload": "u32 mixed add+mul (configs[4])", "global_batch": glob,
-                   "batch_per_gpu": n, "launch_chunk": MIXED_CHUNK, "d": MIXED_PARAMS[0],
+                   "batch_per_gpu": w.n, "launch_chunk": MIXED_CHUNK, "d": MIXED_PARAMS[0],
                    "dp": MIXED_PARAMS[1], "delta": MIXED_PARAMS[2], "tau": MIXED_PARAMS[3],
                    "mul_result_bits": MUL_LOW_K, "parallelism": f"batch-sharded x{world}",
                    "collective": "RCCL all_gather of decrypted results (5 B per value)"},

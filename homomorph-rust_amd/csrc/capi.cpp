@@ -407,8 +407,16 @@ hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     if (enable && c->tev.empty()) {
-        c->tev.resize(2 * kTimedLaunches);
-        for (auto &e : c->tev) HM_HIP(c, hipEventCreate(&e));
+        // created into a local vector and kept only when every event exists
+        std::vector<hipEvent_t> ev(2 * kTimedLaunches, nullptr);
+        for (size_t k = 0; k < ev.size(); ++k) {
+            const hipError_t e = hipEventCreate(&ev[k]);
+            if (e != hipSuccess) {
+                for (size_t j = 0; j < k; ++j) (void)hipEventDestroy(ev[j]);
+                return hip_fail(c, e);
+            }
+        }
+        c->tev.swap(ev);
     }
     c->time_chain = enable != 0;
     c->tev_used = 0;
@@ -680,9 +688,12 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         const uint32_t tiles = (SC + 31) / 32;
         const uint32_t mf_cw = 32 * tiles + 64;
         const uint32_t mf_lds = kMfmaHalo + mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
-        const bool fits = maxPw <= 2 * kMfmaChunks - 1 && cntAB <= 64 &&
+        // x_i below 32 words: the kernel XORs x into sum words 0..31 only (words from 32 up are
+        // the carry's, stored by the tiles), for the last bit as for every other
+        const bool fits = maxPw <= 2 * kMfmaChunks - 1 && cntAB <= 64 && cntX <= 32 &&
                           cntX + cntP + cntAB + 2 <= 64 &&
-                          (256 + (size_t)mf_lds * kAddWavesPerBlock) * 4 <= 160 * 1024;
+                          (256 + (size_t)mf_lds * kAddWavesPerBlock + kMfmaStageWords) * 4 <=
+                              160 * 1024;
         A.mfma = fits && c->add_chain != HM_ADD_CHAIN_VALU;
         if (c->add_chain == HM_ADD_CHAIN_MFMA && !fits) return HM_ERR_UNSUPPORTED;
         if (A.mfma) A.mf_cw = mf_cw, A.chain_lds = mf_lds;

@@ -249,6 +249,8 @@ constexpr int kMfmaChunks = 13;
 constexpr int kMfmaRingSlots = 128;
 constexpr int kMfmaHalo = 32;
 constexpr int kMfmaRsWords = 224; // reversed nibble image of P_i (adder_mfma.hip kRsWords)
+// the chain's static per-block record stage (two 64-word buffers per wave)
+constexpr int kMfmaStageWords = 2 * 64 * kAddWavesPerBlock;
 constexpr size_t kEncTableBytes = 96 * 1024; // largest encryption nibble table staged in LDS
                                               // (tau = 256 at d + dp = 512: 80 KB)
 

@@ -290,46 +290,6 @@ __device__ __forceinline__ int wave_mul(const uint32_t *U, int nu, const uint32_
     return mul_tiles<QC, WMAX, WMAX, PAD>(U, nu, V, nv, Add, nadd, Dst, nout);
 }
 
-// Several waves of a workgroup share one product: output tiles of 64*W words, tile t computed by
-// wave `part` when t % nparts == part.  W is the smallest instantiated width that still gives
-// every wave a tile (capped at WMAX), so small products split too.  Returns the highest set bit
-// of THIS wave's tiles (-1 if none); the caller combines the parts.  Non-PAD operands only.
-// Not called yet: the carry-save kernels still give each product to one wave.  Wiring it in needs
-// a per-workgroup degree reduction after every product.
-template <int QC, int W>
-__device__ __forceinline__ int mul_tiles_split(const uint32_t *U, int nu, const uint32_t *V,
-                                               int nv, const uint32_t *Add, int nadd,
-                                               uint32_t *Dst, int nout, int part, int nparts) {
-    int top = -1;
-    for (int t = part; t * kWave * W < nout; t += nparts) {
-        const int r = t == 0
-            ? mul_tile<W, QC, false, pair_mode<W>(), false>(U, nu, V, nv, Add, nadd, Dst, nout, 0)
-            : mul_tile<W, QC, true, pair_mode<W>(), false>(U, nu, V, nv, Add, nadd, Dst, nout,
-                                                           t * kWave * W);
-        if (r >= 0) top = r; // tiles ascend: the last non-null tile holds the top bit
-    }
-    return top;
-}
-
-template <int QC, int WMAX>
-__device__ __forceinline__ int wave_mul_split(const uint32_t *U, int nu, const uint32_t *V, int nv,
-                                              const uint32_t *Add, int nadd, uint32_t *Dst,
-                                              int *nout_p, int part, int nparts) {
-    nu = (int)rfl((uint32_t)nu), nv = (int)rfl((uint32_t)nv), nadd = (int)rfl((uint32_t)nadd);
-    const int nout = max(nu + nv, nadd);
-    *nout_p = nout;
-    const int w = (nout + kWave * nparts - 1) / (kWave * nparts);
-#define HM_TRY_WS(WW)                                                                             \
-    if constexpr (WW < WMAX) {                                                                    \
-        if (w <= WW) return mul_tiles_split<QC, WW>(U, nu, V, nv, Add, nadd, Dst, nout, part, nparts); \
-    }
-    HM_TRY_WS(1)
-    HM_TRY_WS(2)
-    HM_TRY_WS(4)
-#undef HM_TRY_WS
-    return mul_tiles_split<QC, WMAX>(U, nu, V, nv, Add, nadd, Dst, nout, part, nparts);
-}
-
 // Dst[0..n) = A ^ B (n = max(na, nb)); exact degree (-1 = null).  Strided lane loop.
 __device__ __forceinline__ int wave_xor(const uint32_t *A, int na, const uint32_t *B, int nb,
                                         uint32_t *Dst) {

@@ -64,6 +64,25 @@ def lib():
         L.oracle_set_threads.argtypes = [ctypes.c_int]
         L.oracle_limb_products.restype = ctypes.c_uint64
         L.oracle_reset_counters.restype = None
+        # residue_check.c: the ring-homomorphism checksum (residues mod X^64 + g)
+        L.oracle_residue_threads.restype = None
+        L.oracle_residue_threads.argtypes = [ctypes.c_int]
+        L.oracle_residues.restype = ctypes.c_int
+        L.oracle_residues.argtypes = [u64p, u32p, u32p, ctypes.c_uint32, ctypes.c_size_t,
+                                      ctypes.c_uint64, u64p, szp]
+        L.oracle_residue_add.restype = ctypes.c_int
+        L.oracle_residue_add.argtypes = [u64p, u64p, ctypes.c_uint32, ctypes.c_size_t,
+                                         ctypes.c_uint64, u64p]
+        L.oracle_residue_mul.restype = ctypes.c_int
+        L.oracle_residue_mul.argtypes = [u64p, u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.c_size_t, ctypes.c_uint64, u64p]
+        L.oracle_residue_gate.restype = ctypes.c_int
+        L.oracle_residue_gate.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_size_t,
+                                          ctypes.c_uint64, u64p]
+        L.oracle_residue_of.restype = ctypes.c_uint64
+        L.oracle_residue_of.argtypes = [u64p, ctypes.c_size_t, ctypes.c_uint64]
+        L.oracle_residue_mulmod.restype = ctypes.c_uint64
+        L.oracle_residue_mulmod.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         _lib = L
     return _lib
 
@@ -217,3 +236,58 @@ def limb_products() -> int:
 
 def reset_counters():
     lib().oracle_reset_counters()
+
+
+# ---------------- residue checksum (residue_check.c) ----------------
+# P -> P mod (X^64 + g) is a ring homomorphism, so every circuit output's residue equals the
+# circuit evaluated on the input residues: a size-independent check of whole batches.
+def residues(limbs, deg, bound, nbits, n, g):
+    """(n, nbits) uint64 residues of a batch and the count of degree words that disagree with
+    their limbs (deg may be None: not checked)."""
+    limbs = np.ascontiguousarray(limbs, dtype=np.uint64)
+    bound = np.ascontiguousarray(bound, dtype=np.uint32)
+    dp = None
+    if deg is not None:
+        deg = np.ascontiguousarray(deg, dtype=np.uint32)
+        dp = _p(deg, u32p)
+    out = np.zeros(n * nbits, dtype=np.uint64)
+    bad = ctypes.c_size_t()
+    _check(lib().oracle_residues(_p(limbs, u64p), dp, _p(bound, u32p), nbits, n, g & (2**64 - 1),
+                                 _p(out, u64p), ctypes.byref(bad)), "residues")
+    return out.reshape(n, nbits), int(bad.value)
+
+
+def residue_add(ra, rb, g):
+    ra, rb = np.ascontiguousarray(ra, np.uint64), np.ascontiguousarray(rb, np.uint64)
+    n, nbits = ra.shape
+    out = np.zeros_like(ra)
+    _check(lib().oracle_residue_add(_p(ra, u64p), _p(rb, u64p), nbits, n, g & (2**64 - 1),
+                                    _p(out, u64p)), "residue_add")
+    return out
+
+
+def residue_mul(ra, rb, k, g, signed=False):
+    ra, rb = np.ascontiguousarray(ra, np.uint64), np.ascontiguousarray(rb, np.uint64)
+    n, nbits = ra.shape
+    out = np.zeros((n, k), dtype=np.uint64)
+    _check(lib().oracle_residue_mul(_p(ra, u64p), _p(rb, u64p), nbits, k, int(signed), n,
+                                    g & (2**64 - 1), _p(out, u64p)), "residue_mul")
+    return out
+
+
+def residue_gate(op, ra, rb, g):
+    ra = np.ascontiguousarray(ra, np.uint64)
+    rb = ra if rb is None else np.ascontiguousarray(rb, np.uint64)
+    out = np.zeros_like(ra)
+    _check(lib().oracle_residue_gate(GATES[op], _p(ra, u64p), _p(rb, u64p), ra.size,
+                                     g & (2**64 - 1), _p(out, u64p)), "residue_gate")
+    return out
+
+
+def residue_of(limbs, g) -> int:
+    a = _arr(limbs)
+    return int(lib().oracle_residue_of(_p(a, u64p), a.size, g & (2**64 - 1)))
+
+
+def residue_mulmod(a: int, b: int, g: int) -> int:
+    return int(lib().oracle_residue_mulmod(a, b, g & (2**64 - 1)))

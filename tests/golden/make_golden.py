@@ -44,7 +44,7 @@ CASES = {
     "not_u8_d32": ("not", (32, 16, 16, 16), np.uint8, 2, 110),
     # SURVEY §8(d) configs[3] / row A14: the low 16 result bits of the u32 multiply (the circuit's
     # columns 0..15), stored as degrees + a SHA-256 per value (the outputs are ~200 KB a value)
-    "mullow16_u32_d128": ("mullow16", (128, 128, 1, 128), np.uint32, 2, 111),
+    "mullow16_u32_d128": ("mullow16", (128, 128, 1, 128), np.uint32, 8, 111),
 }
 
 

@@ -140,3 +140,44 @@ def seeded_value_masks(seed, draw, idx, nbits, mask_bytes):
     per = nbits * mask_bytes
     return np.stack([seeded_random_bytes(seed, draw, per, int(e) * per).reshape(nbits, mask_bytes)
                      for e in idx])
+
+
+# ------------------------------------------------------------------ residue checksum
+def residue_modulus(seed):
+    """A random f = X^64 + g for the residue checksum (oracle/residue_check.c)."""
+    return int(np.random.default_rng(seed).integers(0, 2**63, dtype=np.uint64)) * 2 + 1
+
+
+def check_residues(H, op, out, a, b=None, k=None, signed=False, seed=0, chunk=32768):
+    """Every output polynomial of the device batch `out` against the reference circuit `op`
+    ("add", "mul", "and", "or", "xor", "not") run on the residues of the device inputs: P mod f
+    is a ring homomorphism, so residue(out) must equal circuit(residue(a), residue(b)) for every
+    (value, bit), and every degree word must be the exact top bit of its limbs.  Values are
+    copied to the host in chunks.  k: the mul_low result bits (out has k bits).  Returns the
+    number of values checked."""
+    g = residue_modulus(seed)
+    n = out.n
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        al, ad = H.value_slice(a, lo, hi).to_host()
+        ra, bad = oracle.residues(al, ad, a.bound, a.nbits, hi - lo, g)
+        assert bad == 0, f"{op}: {bad} input degree words disagree with their limbs"
+        rb = None
+        if b is not None:
+            bl, bd = H.value_slice(b, lo, hi).to_host()
+            rb, bad = oracle.residues(bl, bd, b.bound, b.nbits, hi - lo, g)
+            assert bad == 0
+        ol, od = H.value_slice(out, lo, hi).to_host()
+        ro, bad = oracle.residues(ol, od, out.bound, out.nbits, hi - lo, g)
+        assert bad == 0, f"{op}: {bad} output degree words disagree with their limbs"
+        if op == "add":
+            want = oracle.residue_add(ra, rb, g)
+        elif op == "mul":
+            want = oracle.residue_mul(ra, rb, k or a.nbits, g, signed=signed)
+        else:
+            want = oracle.residue_gate(op, ra, rb, g)
+        if not np.array_equal(ro, want):
+            e, i = np.argwhere(ro != want)[0]
+            raise AssertionError(f"{op}: residue mismatch at value {lo + e}, bit {i} "
+                                 f"({int((ro != want).sum())} polynomials differ)")
+    return n

@@ -217,6 +217,49 @@ def test_add_edge_values(H, oracle, chain):
     assert np.array_equal(dec, (a.astype(np.uint64) + b) .astype(np.uint32))
 
 
+@pytest.mark.parametrize("chain", ["auto", "mfma", "valu"])
+@pytest.mark.parametrize("skew", ["random", "last_bit_wide"])
+def test_add_skewed_bounds(H, oracle, chain, skew):
+    """Non-uniform per-bit input bounds (capacities above the fresh degree, different for every
+    bit and operand).  "random" keeps P_i within 25 words, so the MFMA chain runs; "last_bit_wide"
+    gives only the last bit a 1100-degree capacity (x_{L-1} of 35 words, past the 32 sum words
+    the MFMA chain XORs x into): the engine must pick the VALU chain on "auto" and refuse a forced
+    MFMA chain, never drop x's upper words."""
+    params = (64, 64, 1, 64)
+    d, dp, delta, tau = params
+    ctx = make_ctx(H, params, 71)
+    ctx.set_add_options(chain)
+    sk, pk, _ = keys(*params, 71)
+    n, nbits = 16, 8
+    rng = np.random.default_rng(72 if skew == "random" else 73)
+    if skew == "random":
+        ba = rng.integers(d + dp, 2 * (d + dp) + 1, size=nbits).astype(np.uint32)
+        bb = rng.integers(d + dp, 2 * (d + dp) + 1, size=nbits).astype(np.uint32)
+    else:
+        ba = np.full(nbits, d + dp, dtype=np.uint32)
+        bb = ba.copy()
+        ba[-1] = 1100
+    a, b = plain(n, np.uint8, 74), plain(n, np.uint8, 75)
+    ma, mb = masks(n, nbits, tau, 76), masks(n, nbits, tau, 77)
+    ca, cb = ctx.encrypt(a, masks=ma, bound=ba), ctx.encrypt(b, masks=mb, bound=bb)
+    if chain == "mfma" and skew == "last_bit_wide":
+        with pytest.raises(H.EngineError):
+            ctx.apply2(H.HomomorphicAddition, ca, cb)
+            ctx.synchronize()
+        return
+    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    dec = ctx.decrypt(cs)
+    ctx.synchronize()
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, ba)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bb)
+    ob = H.add_out_bounds(ba, bb)
+    rl, rd = oracle.add_batch(la, da, ba, lb, db, bb, nbits, n, ob)
+    gl, gd = cs.to_host()
+    assert_batches_equal(gl, gd, rl, rd, ob, n, f"skewed add {skew}/{chain}")
+    rdec = oracle.decrypt_batch(sk, rl, rd, ob, nbits, n).reshape(-1)
+    assert np.array_equal(dec, rdec)
+
+
 def test_add_chain_mfma_unsupported(H):
     """A forced MFMA chain on a plan whose P_i exceeds 25 words is refused, not approximated."""
     params = (256, 256, 1, 256)

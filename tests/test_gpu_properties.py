@@ -11,9 +11,15 @@ properties (the oracle alone would take minutes to hours on the whole batches).
                                                       sampled values bit-exact vs the oracle
   configs[3] u32 mul (low 12 bits), batch 1024        every value's low 12 product bits decrypt
                                                       (up to noise); one value bit-exact
-  configs[4] mixed add + mul-low-8, d=dp=tau=256,     one launch chunk (131072 values, the 8-GPU
-             the per-GPU shard                        shard of 2^20): every value decrypts; two
-                                                      sampled values bit-exact vs the oracle
+  configs[3] u32 mul (low 16 bits), batch 1024        under an S(0) = 0 key every product decrypts
+                                                      to a*b mod 2^16; K = 20 on two values,
+                                                      Karatsuba = schoolbook
+  configs[4] mixed add + mul-low-8, d=dp=tau=256,     the whole 2^20 global batch on one GPU through
+             2^20 values                              bench.py's chunk loop: every value decrypts,
+                                                      8 sampled values bit-exact vs the oracle
+Every full batch is also checked polynomial by polynomial by the residue checksum
+(oracle/residue_check.c, tests/helpers.check_residues): residues mod a random X^64 + g form a
+ring homomorphism, so each output's residue must equal the reference circuit on the inputs'.
 """
 import numpy as np
 import pytest
@@ -89,6 +95,8 @@ def test_add_config1_full_batch(H, oracle):
     assert np.array_equal(dec[idx], rdec)
     # the scheme's own noise flips a handful of sums at these parameters (2 of 4096 in the bench)
     assert len(wrong) < n // 100
+    # every output polynomial of the batch: residue check against the reference's circuit
+    assert helpers.check_residues(H, "add", cs, ca, cb, seed=17) == n
 
 
 def test_bench_inputs_noise_is_the_schemes(H, oracle):
@@ -158,7 +166,8 @@ def test_mul_low12_config3_full_batch(H, oracle):
     sk, pk, _ = keys(*params, 31)
     a, b = plain(n, np.uint32, 32), plain(n, np.uint32, 33)
     ma, mb = masks(n, 32, 128, 34), masks(n, 32, 128, 35)
-    cp = ctx.mul_low(ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb), k)
+    ca_, cb_ = ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb)
+    cp = ctx.mul_low(ca_, cb_, k)
     ctx.synchronize()
     gl, gd = cp.to_host()
     # decrypt the 12-bit result through a 16-bit view whose top 4 bits are null polynomials
@@ -171,6 +180,7 @@ def test_mul_low12_config3_full_batch(H, oracle):
     dec = ctx.decrypt(c16)
     want = ((a.astype(np.uint64) * b) & ((1 << k) - 1)).astype(np.uint16)
     assert np.mean(dec == want) > 0.99
+    assert helpers.check_residues(H, "mul", cp, ca_, cb_, k=k, seed=39) == n
     # one value bit-exact vs the oracle (the k-bit circuit on the low k input bits)
     i = 7
     bound = fresh_bound(128, 128, 32)
@@ -183,28 +193,84 @@ def test_mul_low12_config3_full_batch(H, oracle):
     assert_batches_equal(sl, sd, rl, rd, ob, 1, "config3 sampled")
 
 
-def test_mixed_config4_shard(H, oracle):
-    import torch
-    params, n, k = (256, 256, 1, 256), 131072, 8
-    ctx = make_ctx(H, params, 41)
-    a, b = plain(n, np.uint32, 42), plain(n, np.uint32, 43)
-    ca, cb = ctx.encrypt(a), ctx.encrypt(b)  # device-drawn masks
-    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
+def _s0_zero_seed(params):
+    """A key seed whose secret key has S(0) = 0 (bit 0 of S's first SplitMix64 limb): under such a
+    key (C mod S)(0) = C(0), and evaluation at 0 is a ring homomorphism, so every circuit output
+    decrypts to the plaintext circuit whatever its noise degree (DESIGN.md s6 "scheme noise")."""
+    for seed in range(1, 1000):
+        if not int(keys(*params, seed)[0][0]) & 1:
+            return seed
+    raise AssertionError("no seed")
+
+
+def test_mul_low16_config3_full_batch(H, oracle):
+    """configs[3] (u32 mul, batch 1024) at the bench's K = 16: all 1024 products, under an
+    S(0) = 0 key, decrypt to a*b mod 2^16, and every one of the 1024 x 16 output polynomials
+    passes the residue check against the reference's carry-save circuit."""
+    params, n, k = (128, 128, 1, 128), 1024, 16
+    seed = _s0_zero_seed(params)
+    ctx = make_ctx(H, params, seed)
+    assert not int(ctx.get_secret_key().limbs[0]) & 1
+    a, b = plain(n, np.uint32, 36), plain(n, np.uint32, 37)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)
     cp = ctx.mul_low(ca, cb, k)
-    assert np.array_equal(ctx.decrypt(cs), (a + b).astype(np.uint32))
-    assert np.array_equal(ctx.decrypt(cp, np.uint8), (a.astype(np.uint64) * b % 256).astype(np.uint8))
+    dec = ctx.decrypt(H.pad_bits(cp, 16), np.uint16)
     ctx.synchronize()
-    # two sampled values bit-exact vs the oracle, from the device's own input ciphertexts
-    idx = [5, n - 3]
-    la, da = _rows(H, ca, idx)
-    lb, db = _rows(H, cb, idx)
-    rl, rd = oracle.add_batch(la, da, ca.bound, lb, db, cb.bound, 32, 2, cs.bound)
-    sl, sd = _rows(H, cs, idx)
-    assert_batches_equal(sl, sd, rl, rd, cs.bound, 2, "config4 add sampled")
-    lak, dak, bk = low_bits(la, da, ca.bound, 2, k)
-    lbk, dbk, _ = low_bits(lb, db, cb.bound, 2, k)
-    rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, 2, cp.bound)
-    sl, sd = _rows(H, cp, idx)
-    assert_batches_equal(sl, sd, rl, rd, cp.bound, 2, "config4 mul sampled")
-    del ca, cb, cs, cp
+    want = ((a.astype(np.uint64) * b) & 0xFFFF).astype(np.uint16)
+    assert np.array_equal(dec, want), int(np.sum(dec != want))
+    assert helpers.check_residues(H, "mul", cp, ca, cb, k=k, seed=38) == n
+
+
+def test_mul_low20_karatsuba_vs_schoolbook(H):
+    """K = 20 on two values: the Karatsuba and
+    the schoolbook-only engines give identical ciphertexts, and every output polynomial passes
+    the residue check against the reference's circuit.  (The bit-serial oracle cannot run K = 20
+    in test time; it pins K <= 16 bit for bit.)"""
+    params, n, k = (128, 128, 1, 128), 2, 20
+    ctx = make_ctx(H, params, 97)
+    a, b = plain(n, np.uint32, 98), plain(n, np.uint32, 99)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)
+    ka = ctx.mul_low(ca, cb, k)
+    ctx.synchronize()
+    assert helpers.check_residues(H, "mul", ka, ca, cb, k=k, seed=100) == n
+    ctx.set_mul_options(0, 256)
+    sb = ctx.mul_low(ca, cb, k)
+    ctx.synchronize()
+    kl, kd = ka.to_host()
+    sl, sd = sb.to_host()
+    assert_batches_equal(kl, kd, sl, sd, ka.bound, n, "K=20 karatsuba vs schoolbook")
+
+
+def test_mixed_config4_full_batch(H, oracle):
+    """configs[4] at its full global batch, 2^20 values at d = dp = tau = 256, on one GPU through
+    bench.py's own chunk loop (the N = 1 point of the strong-scaling config): every sum and
+    product decrypts, every output polynomial of all 2^20 values passes the residue check, and 8
+    sampled values are bit-exact vs the oracle."""
+    import torch
+
+    import bench
+    k = bench.MUL_LOW_K
+    w = bench.MixedWorkload(1, 0, None, 1 << 20)
+    w.step()
+    w.ctx.synchronize()
+    ok_s, ok_p, _ = w.verify(None, 0.0)
+    assert ok_s == w.n and ok_p == w.n, (ok_s, ok_p)
+    assert helpers.check_residues(H, "add", w.sums, w.ca, w.cb, seed=44) == w.n
+    assert helpers.check_residues(H, "mul", w.prods, w.ca, w.cb, k=k, seed=45) == w.n
+    idx = np.sort(np.random.default_rng(46).choice(w.n, 8, replace=False))
+    la, da = _rows(H, w.ca, idx)
+    lb, db = _rows(H, w.cb, idx)
+    oracle.set_threads(8)
+    try:
+        rl, rd = oracle.add_batch(la, da, w.ca.bound, lb, db, w.cb.bound, 32, 8, w.sums.bound)
+        sl, sd = _rows(H, w.sums, idx)
+        assert_batches_equal(sl, sd, rl, rd, w.sums.bound, 8, "config4 add sampled")
+        lak, dak, bk = low_bits(la, da, w.ca.bound, 8, k)
+        lbk, dbk, _ = low_bits(lb, db, w.cb.bound, 8, k)
+        rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, 8, w.prods.bound)
+        sl, sd = _rows(H, w.prods, idx)
+        assert_batches_equal(sl, sd, rl, rd, w.prods.bound, 8, "config4 mul sampled")
+    finally:
+        oracle.set_threads(1)
+    del w
     torch.cuda.empty_cache()
