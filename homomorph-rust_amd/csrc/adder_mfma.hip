@@ -34,17 +34,15 @@
 // bit 0 of its f32 encoding is the coefficient.  One v_alignbit per accumulator gathers them.
 #include <hip/hip_runtime.h>
 
-#include "dev_common.h"
+#include "mfma_gf2.h"
 
 namespace hm {
-
-typedef int v8i __attribute__((ext_vector_type(8)));
-// RS: P_i bit-reversed over kRevWords words (> 25), as nibble words, plus the zero nibble words
-// that the windows of the chunks past P reach (j0 + 31 < 32*kRevWords + 32*26)
-constexpr int kRevWords = 28;
-constexpr int kRsWords = 4 * kRevWords + 4 * 26 + 8;
-static_assert(kRsWords <= kMfmaRsWords, "engine.h kMfmaRsWords");
-typedef float v16f __attribute__((ext_vector_type(16)));
+// Per chunk count NC (engine.h MfmaCfg: 13 chunks for P_i up to 25 words, d + d' <= 256; 25 for
+// up to 49 words, d + d' <= 512):
+//   RS    P_i bit-reversed over kRevWords words (> max np + 1), as nibble words, plus the zero
+//         nibble words that the windows of the chunks past P reach;
+//   halo  zero carry words below C (>= the deepest window reach, np words);
+//   rec   words of one bit's workspace record (one or two 64-lane LDS-DMAs).
 
 // Phase timers (tools/chain_check.hip builds with HM_MFMA_PROFILE; the library never does):
 // per-wave sums of s_memtime deltas for the sum store, the A build and the tile loop.
@@ -57,20 +55,6 @@ __device__ unsigned long long *g_mfma_prof; // 4 per wave, set by the harness
 #define HM_PACC(k, a, b)
 #endif
 
-// The lane index as an opaque value: lane-derived addresses computed from it inside the bit loop
-// stay there (hoisted out of it they were live across the whole chain and spilled to scratch,
-// whose reloads then waited on every outstanding global access of the bit)
-__device__ __forceinline__ int lane_opaque() {
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-
-__device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
-    // cbsz = blgp = 4: both operands fp4 e2m1; E8M0 scales 127 = 1.0
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
-}
-
 // acc += A * B over the kMfmaChunks chunks of one tile; rb = the tile's window slot (chunk c's B
 // fragment at rb[2c]).  The reads run kPrefetch chunks ahead of the MFMAs.  Left alone, the
 // compiler hoists all 13 reads (13 x 4 VGPRs beside A's 52: spills) and sinks the MFMAs below
@@ -82,19 +66,19 @@ __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f 
 constexpr int kPrefetch = HM_MFMA_PREFETCH;
 // side(k) runs after MFMA k for k = 1, 4, 7 (the next tile's ring fill in three stages: its LDS
 // latency hides under this tile's MFMAs instead of stalling the wave between tiles)
-template <class Side>
-__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[kMfmaChunks], const uint4 *rb, const uint4 *rbn,
+template <int NC, class Side>
+__device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[NC], const uint4 *rb, const uint4 *rbn,
                                           uint4 (&pf)[kPrefetch], v16f acc, Side &&side) {
     // pf holds this tile's first kPrefetch B fragments (read during the tile before); the last
     // kPrefetch reads of this tile fetch the next tile's (window base rbn; its ring fill is side
     // stage 2, issued above them), so the next tile's first MFMA does not wait for the LDS
-    uint4 bq[kMfmaChunks];
+    uint4 bq[NC];
 #pragma unroll
     for (int c = 0; c < kPrefetch; ++c) bq[c] = pf[c];
 #pragma unroll
-    for (int c = 0; c < kMfmaChunks; ++c) {
-        if (c + kPrefetch < kMfmaChunks) bq[c + kPrefetch] = rb[2 * (c + kPrefetch)];
-        else pf[c + kPrefetch - kMfmaChunks] = rbn[2 * (c + kPrefetch - kMfmaChunks)];
+    for (int c = 0; c < NC; ++c) {
+        if (c + kPrefetch < NC) bq[c + kPrefetch] = rb[2 * (c + kPrefetch)];
+        else pf[c + kPrefetch - NC] = rbn[2 * (c + kPrefetch - NC)];
         const v8i Bf = {(int)bq[c].x, (int)bq[c].y, (int)bq[c].z, (int)bq[c].w, 0, 0, 0, 0};
         acc = mfma_fp4(Af[c], Bf, acc);
         asm volatile("" : "+v"(acc)::"memory");
@@ -131,11 +115,16 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
 constexpr int kMfmaWpb = HM_MFMA_WPB;
 static_assert(kMfmaWpb <= kAddWavesPerBlock, "host LDS plan");
 
-// 4 waves per SIMD (the batch's 4096 waves fill the chip at that): 128 VGPRs
-__global__ void __launch_bounds__(64 * kMfmaWpb) __attribute__((amdgpu_waves_per_eu(4, 4)))
+// NC = 13: 4 waves per SIMD (configs[1]'s 4096 waves fill the chip at that), 128 VGPRs;
+// NC = 25: 2 waves per SIMD, 256 VGPRs (the 25 A fragments alone are 100)
+template <int NC>
+__global__ void __launch_bounds__(64 * kMfmaWpb)
+__attribute__((amdgpu_waves_per_eu(MfmaCfg<NC>::kWavesPerEU, MfmaCfg<NC>::kWavesPerEU)))
 add_chain_mfma_kernel(AddArgs A) {
+    using Cfg = MfmaCfg<NC>;
+    constexpr int kRevWords = Cfg::kRevWords, kRsWords = Cfg::kRsWords, kRec = Cfg::kRecWords;
     extern __shared__ uint32_t lds[];
-    __shared__ uint32_t stage[kMfmaWpb][2][64];
+    __shared__ uint32_t stage[kMfmaWpb][2][kRec];
     uint32_t *tab = lds; // byte -> 8 nibbles, fp4 1.0 (0b0010) per set bit
     for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
         uint32_t v = 0u;
@@ -152,31 +141,32 @@ add_chain_mfma_kernel(AddArgs A) {
     const uint32_t L = A.nbits;
     // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][RS: kRsWords]
     uint32_t *Ls = lds + 256 + (size_t)wave * A.chain_lds;
-    uint32_t *C = Ls + kMfmaHalo;
+    uint32_t *C = Ls + Cfg::kHalo;
     uint32_t *ring = C + A.mf_cw;
     uint32_t *RS = ring + 8 * kMfmaRingSlots;
     const uint32_t *ws = A.ws + e * A.ws_stride;
-    const uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
-    const uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
     uint64_t *po = A.out.limbs + e * A.out.stride;
     uint32_t *dout = A.out.degree + e * L;
     // Bit i's workspace record, copied into stage[wave][i&1] by one LDS-DMA a bit ahead (its
     // latency hides behind the previous bit's tiles): [x_i: cntX][P_i: cntP][ab_i: cntAB][deg P_i]
-    // [deg ab_i] (host plan: at most 64 words).  The DMA is asm: the compiler cannot tell the
+    // [deg ab_i] (host plan: at most kRec words, one DMA per 64).  The DMA is asm: the compiler cannot tell the
     // dynamic LDS from stage and would wait for the DMA before the next LDS write; instead each
     // bit starts with one vmcnt(0), when the DMA and the previous bit's stores are a bit old.
     const uint32_t oP = A.cntX, oAB = oP + A.cntP, oD = oAB + A.cntAB;
-    // lane l's record word of bit i is workspace word lbase + i * lstep (lanes past the record
-    // re-read deg P_i)
-    uint32_t lbase, lstep;
-    {
-        const uint32_t ul = (uint32_t)lane, offD = L * (A.cntAB + A.cntP);
-        if (ul < oP) lbase = offD + 2 * L + ul, lstep = A.cntX;
-        else if (ul < oAB) lbase = L * A.cntAB + (ul - oP), lstep = A.cntP;
-        else if (ul < oD) lbase = ul - oAB, lstep = A.cntAB;
-        else if (ul == oD + 1) lbase = offD, lstep = 1;
-        else lbase = offD + L, lstep = 1;
-    }
+    // record word u of bit i is workspace word base(u) + i * step(u) (words past the record
+    // re-read deg P_i); lane l loads words l and (kRec = 128) 64 + l
+    auto rec_word = [&](uint32_t u, uint32_t &base, uint32_t &step) {
+        const uint32_t offD = L * (A.cntAB + A.cntP);
+        if (u < oP) base = offD + 2 * L + u, step = A.cntX;
+        else if (u < oAB) base = L * A.cntAB + (u - oP), step = A.cntP;
+        else if (u < oD) base = u - oAB, step = A.cntAB;
+        else if (u == oD + 1) base = offD, step = 1;
+        else base = offD + L, step = 1;
+    };
+    uint32_t lbase, lstep, lbase2 = 0, lstep2 = 0;
+    rec_word((uint32_t)lane, lbase, lstep);
+    if constexpr (kRec > 64) rec_word(64u + (uint32_t)lane, lbase2, lstep2);
+    const bool two = kRec > 64 && oD + 2 > 64; // wave-uniform
     const uint64_t wsu = ((uint64_t)rfl((uint32_t)((uintptr_t)ws >> 32)) << 32) |
                          rfl((uint32_t)(uintptr_t)ws); // wave-uniform: SGPR base of the DMA
     auto stage_rec = [&](uint32_t i) {
@@ -186,13 +176,20 @@ add_chain_mfma_kernel(AddArgs A) {
                      :
                      : "v"(voff), "s"(wsu), "s"(m0)
                      : "memory", "m0");
+        if (two) {
+            const uint32_t voff2 = 4u * (lbase2 + i * lstep2);
+            asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                         :
+                         : "v"(voff2), "s"(wsu), "s"(m0 + 256u)
+                         : "memory", "m0");
+        }
     };
     stage_rec(0);
 
 #ifdef HM_MFMA_PROFILE
     unsigned long long prof[3] = {0, 0, 0};
 #endif
-    for (uint32_t k = lane; k < kMfmaHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
+    for (uint32_t k = lane; k < Cfg::kHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
     for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u; // P below bit 0
     wsync();
     int nc = 0;    // carry words (0 = null carry, common.rs:39)
@@ -262,14 +259,14 @@ add_chain_mfma_kernel(AddArgs A) {
         const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
         // A fragments: lane (row m = col, half h), chunk c holds P[s - e], s = 32(D-2c-h) + m,
         // i.e. RS nibbles j0 .. j0+31 with j0 = 32*kRevWords - 1 - s: five words, four funnels
-        // j0 of chunk c = jb + 64c (jb >= 64 since D <= 25 < kRevWords - 1): one base word per
+        // j0 of chunk c = jb + 64c (jb >= 64 since D <= 2 NC - 1 < kRevWords - 2): one base word per
         // lane, chunk c at +8c words (immediate offsets), one shift for all chunks
-        v8i Af[kMfmaChunks];
+        v8i Af[NC];
         const int jb = 32 * (kRevWords - D + h) - 1 - col;
         const uint32_t *rw0 = RS + (jb >> 3);
         const uint32_t sh = 4u * (uint32_t)(jb & 7);
 #pragma unroll
-        for (int c = 0; c < kMfmaChunks; ++c) {
+        for (int c = 0; c < NC; ++c) {
             const uint32_t *rw = rw0 + 8 * c;
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3], w4 = rw[4];
             Af[c] = (v8i){(int)funnel(w1, w0, sh), (int)funnel(w2, w1, sh), (int)funnel(w3, w2, sh),
@@ -284,7 +281,8 @@ add_chain_mfma_kernel(AddArgs A) {
         uint32_t *son = (uint32_t *)(po + offo);
         const int capn = 2 * (int)cap_of(A.ob.b[i + 1]);
         const int wlo = 32;
-        ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 64, lane);
+        // the top tile's whole window: words 32(tiles-1) - D .. + 32 + 2 NC
+        ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 32 + 2 * NC, lane);
         int ldeg = -1;
         // The accumulators start at 2^23 once per bit and keep accumulating tile after tile
         // (2^23 + every count stays below 2^24, exact): a tile's parities are bit 0 of its
@@ -313,7 +311,7 @@ add_chain_mfma_kernel(AddArgs A) {
             const int W = 32 * T + col;
             const uint32_t abw = W < nab ? abi[W] : 0u;
             __builtin_amdgcn_s_setprio(1); // the MFMA phase keeps the pipe
-            acc = tile_mfma(Af, rb, rbn, pf, acc, [&](int stage) {
+            acc = tile_mfma<NC>(Af, rb, rbn, pf, acc, [&](int stage) {
                 if (T == 0) return;
                 // (the empty asm keep each stage's arithmetic from being hoisted into an earlier
                 // stage, where it would wait for the read of the stage before)
@@ -373,8 +371,14 @@ int launch_add_chain_mfma(const AddArgs &a, void *stream) {
     const int wpb = kMfmaWpb;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     const size_t lds = (256 + (size_t)a.chain_lds * wpb) * 4;
-    hipLaunchKernelGGL(add_chain_mfma_kernel, dim3((unsigned)blocks), dim3(64 * wpb), lds,
-                       (hipStream_t)stream, a);
+    if (a.mfma == MfmaCfg<13>::kChunks)
+        hipLaunchKernelGGL(add_chain_mfma_kernel<13>, dim3((unsigned)blocks), dim3(64 * wpb), lds,
+                           (hipStream_t)stream, a);
+    else if (a.mfma == MfmaCfg<25>::kChunks)
+        hipLaunchKernelGGL(add_chain_mfma_kernel<25>, dim3((unsigned)blocks), dim3(64 * wpb), lds,
+                           (hipStream_t)stream, a);
+    else
+        return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

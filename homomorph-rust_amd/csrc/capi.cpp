@@ -445,9 +445,15 @@ hm_status hm_ctx_set_add_options(hm_ctx *c, uint32_t chain) {
 }
 
 hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) {
-    if (!c || (ka_min && (ka_leaf < 32 || ka_leaf > 384))) return HM_ERR_INVALID_ARGUMENT;
+    if (!c || (ka_min && (ka_leaf < 32 || ka_leaf > 512))) return HM_ERR_INVALID_ARGUMENT;
     c->ka_min = ka_min;
     c->ka_leaf = ka_leaf & ~31u;
+    return HM_OK;
+}
+
+hm_status hm_ctx_set_mul_products(hm_ctx *c, uint32_t products) {
+    if (!c || products > HM_MUL_PRODUCTS_VALU) return HM_ERR_INVALID_ARGUMENT;
+    c->mul_products = products;
     return HM_OK;
 }
 
@@ -687,16 +693,26 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     {
         const uint32_t tiles = (SC + 31) / 32;
         const uint32_t mf_cw = 32 * tiles + 64;
-        const uint32_t mf_lds = kMfmaHalo + mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
-        // x_i below 32 words: the kernel XORs x into sum words 0..31 only (words from 32 up are
-        // the carry's, stored by the tiles), for the last bit as for every other
-        const bool fits = maxPw <= 2 * kMfmaChunks - 1 && cntAB <= 64 && cntX <= 32 &&
-                          cntX + cntP + cntAB + 2 <= 64 &&
-                          (256 + (size_t)mf_lds * kAddWavesPerBlock + kMfmaStageWords) * 4 <=
-                              160 * 1024;
-        A.mfma = fits && c->add_chain != HM_ADD_CHAIN_VALU;
-        if (c->add_chain == HM_ADD_CHAIN_MFMA && !fits) return HM_ERR_UNSUPPORTED;
-        if (A.mfma) A.mf_cw = mf_cw, A.chain_lds = mf_lds;
+        // the smallest chunk count whose plan fits: P_i within 2 NC - 1 words, ab_i within 64
+        // words (two tiles), the bit's record within kRecWords, and x_i below 32 words (the
+        // kernel XORs x into sum words 0..31 only; words from 32 up are the carry's, stored by the
+        // tiles), for the last bit as for every other; LDS (dynamic + the static record stage)
+        // for one block
+        auto plan = [&](auto cfg) -> uint32_t {
+            using Cfg = decltype(cfg);
+            const uint32_t lds = Cfg::kHalo + mf_cw + 8 * kMfmaRingSlots + Cfg::kRsWords;
+            const bool fits = maxPw <= 2 * Cfg::kChunks - 1 && cntAB <= 64 && cntX <= 32 &&
+                              cntX + cntP + cntAB + 2 <= (uint32_t)Cfg::kRecWords &&
+                              (256 + (size_t)lds * kAddWavesPerBlock + Cfg::kStageWords) * 4 <=
+                                  160 * 1024;
+            return fits ? lds : 0u;
+        };
+        uint32_t nc = 0, lds = 0;
+        if ((lds = plan(MfmaCfg<13>{}))) nc = 13;
+        else if ((lds = plan(MfmaCfg<25>{}))) nc = 25;
+        A.mfma = c->add_chain != HM_ADD_CHAIN_VALU ? nc : 0u;
+        if (c->add_chain == HM_ADD_CHAIN_MFMA && !nc) return HM_ERR_UNSUPPORTED;
+        if (A.mfma) A.mf_cw = mf_cw, A.chain_lds = lds;
     }
     A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
     const size_t bytes = (size_t)A.ws_stride * 4 * a->n;

@@ -64,6 +64,8 @@ struct hm_ctx {
     // Karatsuba carry products (hm_ctx_set_mul_options): shorter operand >= ka_min words (0 =
     // never), recursion down to leaves of at most ka_leaf words
     uint32_t ka_min = 1024, ka_leaf = 256;
+    // where the Karatsuba leaf products run (hm_ctx_set_mul_products): HM_MUL_PRODUCTS_*
+    uint32_t mul_products = 0;
     // carry chain of the adder (hm_ctx_set_add_options): HM_ADD_CHAIN_AUTO / _MFMA / _VALU
     uint32_t add_chain = 0;
     // per-launch timing of the adder's carry-chain kernel (hm_ctx_set_kernel_timing): a pair of

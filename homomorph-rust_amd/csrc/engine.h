@@ -40,7 +40,8 @@ struct AddArgs {
     uint32_t cw;                      // chain: carry buffer words
     uint32_t max_prod_words;          // widest carry product along the chain (picks WMAX)
     uint32_t pad;                     // carry buffers zero-padded: unchecked window reads (see capi)
-    uint32_t mfma;                    // chain on the matrix cores (adder_mfma.hip)
+    uint32_t mfma;                    // chain on the matrix cores (adder_mfma.hip): its chunk count
+                                      // NC (MfmaCfg), 0 = the VALU chain
     uint32_t mf_cw;                   // MFMA chain: carry bit words (tiles, window overhang)
     int *status;
     Bounds ab, bb, ob;
@@ -172,6 +173,15 @@ struct MulVProdArgs {
     const MulVTile *tiles;
     uint32_t ntiles;
 };
+// the same leaf products on the matrix cores (mul_mfma.hip): one wave per (value, task), LDS
+// slices of wave_words words (operand images and the output, sized by the launch's largest
+// operands umax, vmax and output omax)
+struct MulLeafArgs {
+    MulBase B;
+    const MulVTask *tasks;
+    uint32_t ntasks;
+    uint32_t umax, vmax, omax, wave_words;
+};
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
 struct KaComb {
     uint32_t z0, z1, z2; // child results, 2h words each (z1 may be kKaNone)
@@ -234,6 +244,8 @@ int launch_mul_prod(const MulProdArgs &a, uint32_t w, void *stream);
 int launch_mul_final(const MulFinalArgs &a, void *stream);
 int launch_ka_sum(const KaSumArgs &a, void *stream);
 int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
+int launch_mul_leaf_mfma(const MulLeafArgs &a, void *stream);
+uint32_t mul_leaf_wave_words(uint32_t umax, uint32_t vmax, uint32_t omax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);
 int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches
@@ -243,14 +255,22 @@ int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *
 
 constexpr int kAddWavesPerBlock = 4;
 constexpr size_t kTimedLaunches = 4096; // chain launches hm_ctx_set_kernel_timing can record
-// MFMA carry chain (adder_mfma.hip): P_i within 2*kMfmaChunks-1 words, nibble ring slots (a power
-// of two above the 58-word window of a tile plus the 32 words filled ahead), zero words below C
-constexpr int kMfmaChunks = 13;
+// MFMA carry chain (adder_mfma.hip), one configuration per chunk count NC: P_i within 2 NC - 1
+// words (NC = 13: 25 words, d + d' <= 256; NC = 25: 49 words, d + d' <= 512), nibble ring slots
+// (a power of two above a tile's 32 + 2 NC word window plus the 32 words filled ahead), zero carry
+// words below C (the deepest window reach), a bit's workspace record in one or two 64-word
+// LDS-DMAs, and the SIMD occupancy the A fragments (4 NC VGPRs) leave.
 constexpr int kMfmaRingSlots = 128;
-constexpr int kMfmaHalo = 32;
-constexpr int kMfmaRsWords = 224; // reversed nibble image of P_i (adder_mfma.hip kRsWords)
-// the chain's static per-block record stage (two 64-word buffers per wave)
-constexpr int kMfmaStageWords = 2 * 64 * kAddWavesPerBlock;
+template <int NC> struct MfmaCfg {
+    static constexpr int kChunks = NC;
+    static constexpr int kRevWords = 2 * NC + 2;            // > max np + 1 (jb >= 64)
+    static constexpr int kRsWords = 4 * kRevWords + 8 * NC + 8;
+    static constexpr int kHalo = NC <= 16 ? 32 : 64;        // >= 2 NC - 1
+    static constexpr int kRecWords = NC <= 16 ? 64 : 128;
+    static constexpr int kWavesPerEU = NC <= 16 ? 4 : 2;
+    static constexpr int kStageWords = 2 * kRecWords * kAddWavesPerBlock; // static LDS per block
+    static_assert(32 + 2 * NC + 32 <= kMfmaRingSlots, "ring window");
+};
 constexpr size_t kEncTableBytes = 96 * 1024; // largest encryption nibble table staged in LDS
                                               // (tau = 256 at d + dp = 512: 80 KB)
 

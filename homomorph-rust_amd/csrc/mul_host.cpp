@@ -43,6 +43,7 @@ struct KaProg {
     uint32_t u, v, out;                          // slots (exact degrees: deg1)
     std::vector<std::array<uint32_t, 3>> sums;   // per level 1..k: (first KaSum, count, h)
     uint32_t vtask = 0, nvtask = 0;              // leaf products (MulVTask range)
+    uint32_t leaf_umax = 0, leaf_vmax = 0, leaf_omax = 0; // their largest operands and output
     uint32_t tiles[kNW] = {}, ntiles[kNW] = {};  // their tiles (MulVTile ranges) per width class
     std::vector<std::array<uint32_t, 3>> combs;  // per level k..1: (first KaComb, count, h)
 };
@@ -271,6 +272,11 @@ bool build_plan(MulPlan &P) {
                 P.ka_sums.insert(P.ka_sums.end(), kb.sums[l].begin(), kb.sums[l].end());
             }
             pg.vtask = (uint32_t)P.ka_vtasks.size(), pg.nvtask = (uint32_t)kb.leaves.size();
+            for (const MulVTask &t : kb.leaves) {
+                pg.leaf_umax = std::max(pg.leaf_umax, t.nu);
+                pg.leaf_vmax = std::max(pg.leaf_vmax, t.nv);
+                pg.leaf_omax = std::max(pg.leaf_omax, t.nout);
+            }
             P.ka_vtasks.insert(P.ka_vtasks.end(), kb.leaves.begin(), kb.leaves.end());
             uint32_t wc = kNW - 1;
             for (uint32_t q = 0; q < kNW; ++q)
@@ -460,12 +466,21 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         a.B = B, a.t = (const KaSum *)(T + P.off_ka_sums) + lv[0], a.nt = lv[1], a.h = lv[2];
         if (launch_ka_sum(a, c->stream)) return hip_fail(c, hipGetLastError());
     }
-    for (uint32_t q = 0; q < kNW; ++q) {
-        if (!pg.ntiles[q]) continue;
-        MulVProdArgs a{};
-        a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
-        a.tiles = (const MulVTile *)(T + P.off_ka_vtiles) + pg.tiles[q], a.ntiles = pg.ntiles[q];
-        if (launch_mul_vprod(a, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
+    if (c->mul_products != HM_MUL_PRODUCTS_VALU) {
+        // the leaves on the matrix cores: one wave per (value, leaf)
+        MulLeafArgs a{};
+        a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask, a.ntasks = pg.nvtask;
+        a.umax = pg.leaf_umax, a.vmax = pg.leaf_vmax, a.omax = pg.leaf_omax;
+        a.wave_words = mul_leaf_wave_words(a.umax, a.vmax, a.omax);
+        if (launch_mul_leaf_mfma(a, c->stream)) return hip_fail(c, hipGetLastError());
+    } else {
+        for (uint32_t q = 0; q < kNW; ++q) {
+            if (!pg.ntiles[q]) continue;
+            MulVProdArgs a{};
+            a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
+            a.tiles = (const MulVTile *)(T + P.off_ka_vtiles) + pg.tiles[q], a.ntiles = pg.ntiles[q];
+            if (launch_mul_vprod(a, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
+        }
     }
     for (const auto &lv : pg.combs) {
         KaCombArgs a{};

@@ -458,6 +458,15 @@ class Context:
         _check(lib().hm_ctx_set_mul_options(self._h, karatsuba_min_words, karatsuba_leaf_words),
                "hm_ctx_set_mul_options")
 
+    MUL_PRODUCTS = {"auto": 0, "mfma": 1, "valu": 2}
+
+    def set_mul_products(self, products: str = "auto"):
+        """hm_ctx_set_mul_products: where the multiplier's Karatsuba leaf products run -- "mfma"
+        (fp4 matrix cores, {0,1} Toeplitz GEMMs reduced mod 2; the default, "auto") or "valu"
+        (scalar-decided XORs).  Results are identical either way (every product is exact)."""
+        _check(lib().hm_ctx_set_mul_products(self._h, self.MUL_PRODUCTS[products]),
+               "hm_ctx_set_mul_products")
+
     def generation(self) -> int:
         return int(lib().hm_ctx_generation(self._h))
 

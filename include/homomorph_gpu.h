@@ -151,15 +151,23 @@ hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
 /* Multiplier strategy (no effect on results: every product is exact).  A carry product of the
  * carry-save circuit whose shorter operand has at least karatsuba_min_words 32-bit words runs as
  * a Karatsuba recursion down to leaves of at most karatsuba_leaf_words
- * words (rounded to a multiple of 32); smaller products run as schoolbook tiles.
+ * words (rounded to a multiple of 32, at most 512); smaller products run as schoolbook tiles.
  * karatsuba_min_words = 0 disables it.  Defaults: 1024 and 256. */
 hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
                                  uint32_t karatsuba_leaf_words);
 
+/* Where the multiplier's Karatsuba leaf products run (no effect on results: every product is
+ * exact): as {0,1} Toeplitz GEMMs on the fp4 matrix cores (MFMA, reduced mod 2) or as
+ * scalar-decided VALU XORs.  AUTO = MFMA. */
+#define HM_MUL_PRODUCTS_AUTO 0u
+#define HM_MUL_PRODUCTS_MFMA 1u
+#define HM_MUL_PRODUCTS_VALU 2u
+hm_status hm_ctx_set_mul_products(hm_ctx *ctx, uint32_t products);
+
 /* Adder strategy (no effect on results: both chains are exact).  The carry chain
  * carry' = ab_i ^ P_i * carry (src/impls/numbers/common.rs:37-56) runs its products either on the
- * matrix cores (a {0,1} Toeplitz product on fp4 MFMA, reduced mod 2; needs P_i within 25 words,
- * i.e. d + dp <= 256 for u32) or as scalar-decided VALU XORs.  AUTO picks the MFMA chain when it
+ * matrix cores (a {0,1} Toeplitz product on fp4 MFMA, reduced mod 2; needs P_i within 49 words,
+ * i.e. d + dp <= 512 for u32) or as scalar-decided VALU XORs.  AUTO picks the MFMA chain when it
  * applies; MFMA on a plan it cannot run returns HM_ERR_UNSUPPORTED at hm_add_batch. */
 #define HM_ADD_CHAIN_AUTO 0u
 #define HM_ADD_CHAIN_MFMA 1u

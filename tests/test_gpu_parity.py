@@ -155,7 +155,7 @@ def _pair(H, ctx, params, dtype, n, seed, lo=None, hi=None):
     return a, b, ma, mb, ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb)
 
 
-@pytest.mark.parametrize("chain", ["auto", "valu"])
+@pytest.mark.parametrize("chain", ["auto", "mfma", "valu"])
 @pytest.mark.parametrize("params,dtype,n", [((64, 64, 1, 64), np.uint8, 128),
                                             ((64, 64, 1, 64), np.uint32, 32),
                                             ((64, 16, 1, 16), np.uint8, 64),
@@ -165,7 +165,8 @@ def _pair(H, ctx, params, dtype, n, seed, lo=None, hi=None):
                                             ((256, 128, 1, 128), np.uint64, 2)])
 def test_add_parity(H, oracle, params, dtype, n, chain):
     """Both carry chains (fp4 MFMA Toeplitz products and VALU XORs) against the oracle.  "auto"
-    runs the MFMA chain wherever P_i fits 25 words (d + dp <= 256 here), the VALU chain above."""
+    and "mfma" run the MFMA chain: 13 chunks where P_i fits 25 words (d + dp <= 256), 25 chunks
+    up to 49 words (d + dp = 512 here)."""
     d, dp, delta, tau = params
     ctx = make_ctx(H, params, 17)
     ctx.set_add_options(chain)
@@ -261,11 +262,12 @@ def test_add_skewed_bounds(H, oracle, chain, skew):
 
 
 def test_add_chain_mfma_unsupported(H):
-    """A forced MFMA chain on a plan whose P_i exceeds 25 words is refused, not approximated."""
-    params = (256, 256, 1, 256)
+    """A forced MFMA chain on a plan whose P_i exceeds 49 words (d + dp = 1024: 97 words) is
+    refused, not approximated."""
+    params = (768, 256, 1, 64)
     ctx = make_ctx(H, params, 3)
     ctx.set_add_options("mfma")
-    a = ctx.encrypt(np.array([1, 2], dtype=np.uint8), masks=masks(2, 8, 256, 1))
+    a = ctx.encrypt(np.array([1, 2], dtype=np.uint8), masks=masks(2, 8, 64, 1))
     with pytest.raises(H.EngineError):
         ctx.apply2(H.HomomorphicAddition, a, a)
         ctx.synchronize()
@@ -404,15 +406,18 @@ def test_mul_low_parity(H, oracle, k, n):
         assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("ka_min,leaf", [(32, 32), (64, 96), (128, 256)])
-def test_mul_karatsuba_parity(H, oracle, ka_min, leaf):
+@pytest.mark.parametrize("products", ["mfma", "valu"])
+@pytest.mark.parametrize("ka_min,leaf", [(32, 32), (64, 96), (128, 256), (256, 512)])
+def test_mul_karatsuba_parity(H, oracle, ka_min, leaf, products):
     """The Karatsuba carry products (hm_ctx_set_mul_options) forced down
-    to small sizes: u8 multiply and the u32 low-12 prefix, bit-exact vs the oracle's bit-serial
-    products, and equal to the schoolbook-only engine (karatsuba_min_words = 0)."""
+    to small sizes, their leaves on the fp4 matrix cores or as VALU XORs (hm_ctx_set_mul_products):
+    u8 multiply and the u32 low-12 prefix, bit-exact vs the oracle's bit-serial products, and equal
+    to the schoolbook-only engine (karatsuba_min_words = 0)."""
     from helpers import low_bits
     params = (128, 128, 1, 128)
     ctx = make_ctx(H, params, 91)
     ctx.set_mul_options(ka_min, leaf)
+    ctx.set_mul_products(products)
     sk, pk, _ = keys(*params, 91)
     bound = fresh_bound(128, 128, 32)
     # u8: products up to ~450 words
@@ -453,11 +458,16 @@ def test_mul_karatsuba_low16_matches_schoolbook(H):
     ca, cb = ctx.encrypt(x), ctx.encrypt(x[::-1].copy())
     ka = ctx.mul_low(ca, cb, 16)
     ctx.synchronize()
+    ctx.set_mul_products("valu")
+    kv = ctx.mul_low(ca, cb, 16)
+    ctx.synchronize()
     ctx.set_mul_options(0, 256)
     sb = ctx.mul_low(ca, cb, 16)
     ctx.synchronize()
     kl, kd = ka.to_host()
+    vl, vd = kv.to_host()
     sl, sd = sb.to_host()
+    assert_batches_equal(kl, kd, vl, vd, ka.bound, 3, "K=16 MFMA leaves vs VALU leaves")
     assert_batches_equal(kl, kd, sl, sd, ka.bound, 3, "K=16 karatsuba vs schoolbook")
 
 

@@ -33,17 +33,23 @@ static int degp1(const uint32_t *w, int n) {
 
 static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool quiet);
 
-static int timing(int nvals);
+static int timing(int nvals, bool wide);
 
 int main(int argc, char **argv) {
-    if (argc > 1 && !strcmp(argv[1], "time")) return timing(argc > 2 ? atoi(argv[2]) : 4096);
-    if (argc > 1 && !strcmp(argv[1], "sweep")) {
-        const int ps[] = {0, 5, 31, 32, 100, 400, 650, 700, 736, 767};
+    if (argc > 1 && !strcmp(argv[1], "time")) return timing(argc > 2 ? atoi(argv[2]) : 4096, false);
+    if (argc > 1 && !strcmp(argv[1], "time25")) return timing(argc > 2 ? atoi(argv[2]) : 131072, true);
+    if (argc > 1 && (!strcmp(argv[1], "sweep") || !strcmp(argv[1], "sweep25"))) {
+        // single set bits of P_1 and carry_1 at chosen positions (NC = 13: P of 24 words;
+        // sweep25: NC = 25, P of 49 words, ab of 33)
+        const bool w = !strcmp(argv[1], "sweep25");
+        const int ps13[] = {0, 5, 31, 32, 100, 400, 650, 700, 736, 767};
+        const int ps25[] = {0, 5, 31, 32, 100, 700, 800, 1100, 1500, 1567};
         const int cs[] = {0, 7, 31, 32, 100, 300, 480, 511};
+        const int *ps = w ? ps25 : ps13;
         int nbad = 0;
-        for (int pb : ps)
+        for (int q = 0; q < 10; ++q)
             for (int cb : cs)
-                if (run_case(3, 24, 16, 1, pb, cb, true)) {
+                if (const int pb = ps[q]; run_case(3, w ? 49 : 24, w ? 33 : 16, 1, pb, cb, true)) {
                     const int o = pb + cb;
                     printf("FAIL p=%d c=%d -> out bit %d (W=%d m=%d, cword=%d, pword=%d)\n", pb, cb, o, o / 32, o % 32, cb / 32, pb / 32);
                     ++nbad;
@@ -105,8 +111,10 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     A.out.stride = (uint64_t)outcap * L;
     const uint32_t tiles = (uint32_t)((maxw + 31) / 32) + 1;
     A.mf_cw = 32 * tiles + 64;
-    A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
-    A.mfma = 1;
+    A.mfma = npw <= 25 ? 13 : 25;
+    A.chain_lds = (A.mfma == 13 ? MfmaCfg<13>::kHalo + MfmaCfg<13>::kRsWords
+                                : MfmaCfg<25>::kHalo + MfmaCfg<25>::kRsWords) +
+                  A.mf_cw + 8 * kMfmaRingSlots;
     uint32_t *dws;
     uint64_t *dout;
     uint32_t *ddeg;
@@ -159,11 +167,13 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     return bad;
 }
 
-// configs[1]-shaped chain (32 bits, P 25 words, ab 17 words, x 9 words) replicated over nvals
-// values: kernel time and per-phase s_memtime sums (cycles summed over waves)
-static int timing(int nvals) {
+// configs[1]-shaped chain (32 bits, P 25 words, ab 17 words, x 9 words; wide: configs[4]'s,
+// P 49, ab 33, x 17) replicated over nvals values: kernel time and per-phase s_memtime sums
+// (cycles summed over waves)
+static int timing(int nvals, bool wide) {
     const int L = 32;
-    const uint32_t cntAB = 17, cntP = 25, cntX = 9;
+    const uint32_t cntAB = wide ? 33 : 17, cntP = wide ? 49 : 25, cntX = wide ? 17 : 9;
+    const uint32_t D = wide ? 512 : 256;
     std::mt19937_64 rng(11);
     AddArgs A{};
     A.n = (uint64_t)nvals, A.nbits = L, A.cntAB = cntAB, A.cntP = cntP, A.cntX = cntX;
@@ -180,18 +190,20 @@ static int timing(int nvals) {
             for (uint32_t k = 0; k < cntX; ++k) w[L * (cntAB + cntP + 2) + i * cntX + k] = (uint32_t)rng() & (k + 1 < cntX ? ~0u : 1u);
         }
     }
-    const uint32_t maxw = 25 * L + 40;
-    // the add's output bounds at d + d' = 256 (hm_add_out_bounds): s_0 <= 256, s_i <= (3i-1)*256
+    const uint32_t maxw = cntP * L + 40;
+    // the add's output bounds (hm_add_out_bounds): s_0 <= D, s_i <= (3i-1) D
     uint64_t stride = 0;
     for (int i = 0; i < L; ++i) {
-        A.ob.b[i] = i == 0 ? 256u : (uint32_t)(3 * i - 1) * 256u;
+        A.ob.b[i] = i == 0 ? D : (uint32_t)(3 * i - 1) * D;
         stride += A.ob.b[i] / 64 + 1;
     }
     A.out.stride = stride;
     const uint32_t tiles = (maxw + 31) / 32;
     A.mf_cw = 32 * tiles + 64;
-    A.chain_lds = kMfmaHalo + A.mf_cw + 8 * kMfmaRingSlots + kMfmaRsWords;
-    A.mfma = 1;
+    A.mfma = wide ? 25 : 13;
+    A.chain_lds = (wide ? MfmaCfg<25>::kHalo + MfmaCfg<25>::kRsWords
+                        : MfmaCfg<13>::kHalo + MfmaCfg<13>::kRsWords) +
+                  A.mf_cw + 8 * kMfmaRingSlots;
     uint32_t *dws, *ddeg;
     uint64_t *dout;
     int *dst;
@@ -210,9 +222,9 @@ static int timing(int nvals) {
     hipMemcpyToSymbol(HIP_SYMBOL(g_mfma_prof), &dprof, sizeof dprof);
 #endif
     // ~0.3 s of launches first: the clock ramps up under load (MI355X_MICROARCH.md DVFS)
-    for (int r = 0; r < 300; ++r) launch_add_chain_mfma(A, nullptr);
+    for (int r = 0; r < (wide ? 20 : 300); ++r) launch_add_chain_mfma(A, nullptr);
     hipDeviceSynchronize();
-    const int reps = 50;
+    const int reps = wide ? 5 : 50;
     hipEventRecord(e0);
     for (int r = 0; r < reps; ++r) launch_add_chain_mfma(A, nullptr);
     hipEventRecord(e1);
