@@ -297,38 +297,109 @@ def confirm_noise(ctx, a, b, ca, cb, out, got):
     return res
 
 
-def secondary_metrics(ctx, device, steps):
+def oracle_leg(fn, per_call, seconds, what):
+    """The oracle (C restatement of the reference's path) on ONE host thread, as the reference
+    runs: fn() repeated for about `seconds`, per_call units each.  A baseline, not a target."""
+    from oracle import oracle_py as oracle
+    oracle.set_threads(1)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        done += per_call
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "cores": 1, "kind": "port", "cpu": cpu_model(),
+            "sample": f"{done} {what} in {el:.2f} s on 1 thread (C oracle, -O3)"}
+
+
+def hbm_roofline(alg_bytes, seconds, kernel, note):
+    achieved = alg_bytes / seconds / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "kernel": kernel, "note": note}
+
+
+def s0_zero_context(device, params=PARAMS):
+    """A seeded context whose secret key has S(0) = 0: (C mod S)(0) = C(0) and evaluation at 0 is a
+    ring homomorphism, so every circuit output decrypts whatever its noise degree (DESIGN.md s6);
+    the multiply lines use it so that their decrypt check covers every product."""
+    for seed in range(BENCH_SEED, BENCH_SEED + 64):
+        ctx = H.Context(H.Parameters(*params), device=device)
+        ctx.seed_rng(seed)
+        ctx.generate_secret_key()
+        if not int(ctx.get_secret_key().limbs[0]) & 1:
+            ctx.generate_public_key()
+            return ctx, seed
+    raise RuntimeError("no S(0) = 0 seed")
+
+
+def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
+    """The other BASELINE configs and the README's other published timings (README.md:73-77,
+    benches/u32.rs:17-23, 47-49), each with the oracle's single-thread CPU rate beside it."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     out = {}
+    L = H.lib()
+    leg_s = max(1.0, cpu_seconds / 6)
     # configs[2]: u32 encrypt + decrypt, batch 65536.  Like the reference (whose encryption
     # draws its subset masks from getrandom), each step draws fresh masks from the engine's
     # CSPRNG (device ChaCha20) inside the timed step; the same pair over pre-drawn masks is
-    # reported beside it.
+    # reported beside it.  Encryption and decryption alone are timed the same way.
     n = 65536
-    vals = torch.from_numpy(np.random.default_rng(7).integers(0, 2**32, size=n, dtype=np.uint32)
-                            .view(np.int32)).to(device)
+    vals_np = np.random.default_rng(7).integers(0, 2**32, size=n, dtype=np.uint32)
+    vals = torch.from_numpy(vals_np.view(np.int32)).to(device)
     data = vals.view(torch.uint8).reshape(n, 4)
     m = ctx.random_bytes(n * 32 * ctx.mask_bytes())
     bound = np.full(32, ctx.fresh_bound(), dtype=np.uint32)
     c = H.Ciphered.empty(n, bound, device)
     dec = torch.empty((n, 4), dtype=torch.uint8, device=device)
     cb = c._c()
-    L = H.lib()
-    import ctypes
 
-    def encdec(masks_ptr):
+    def enc(masks_ptr):
         ctx._launch(lambda: L.hm_encrypt_batch(ctx._h, data.data_ptr(), 4, masks_ptr,
-                                               ctypes.byref(cb))
-                    | L.hm_decrypt_batch(ctx._h, ctypes.byref(cb), dec.data_ptr()), "enc+dec")
+                                               ctypes.byref(cb)), "encrypt")
+
+    def decr():
+        ctx._launch(lambda: L.hm_decrypt_batch(ctx._h, ctypes.byref(cb), dec.data_ptr()), "decrypt")
 
     reps = max(20, 5 * steps)
+
+    def timed(fn):
+        # launch-bound (tens of us of kernels): replayed as one captured HIP graph per step
+        g = ctx.graph(fn, warmup=2)
+        wall, ev_s = time_loop(g.replay, reps, 2, 1)  # replays run on the current stream
+        ctx.synchronize()
+        return n * reps / wall, ev_s / reps
+
     res = {}
     for key, mp in (("csprng", None), ("predrawn", m.data_ptr())):
-        # the pair is launch-bound (~65 us of kernels): replay it as one captured HIP graph
-        g = ctx.graph(lambda: encdec(mp), warmup=2)
         dec.zero_()
-        wall, ev_s = time_loop(g.replay, reps, 2, 1)
-        ctx.synchronize()
-        res[key] = (n * reps / wall, bool(torch.equal(dec, data)), 1e6 * ev_s / reps)
+        r, ks = timed(lambda: (enc(mp), decr()))
+        res[key] = (r, bool(torch.equal(dec, data)), 1e6 * ks)
+    enc_r, enc_k = timed(lambda: enc(m.data_ptr()))
+    encc_r, encc_k = timed(lambda: enc(None))
+    enc(m.data_ptr())
+    dec.zero_()
+    dec_r, dec_k = timed(decr)
+    dec_ok = bool(torch.equal(dec, data))
+    ctx.synchronize()
+
+    from helpers import as_bytes, masks as hmasks
+    from oracle import oracle_py as oracle
+    sk, pk = ctx.get_secret_key().limbs, ctx.get_public_key().limbs
+    ns = 64
+    xs = vals_np[:ns]
+    ms = hmasks(ns, 32, PARAMS[3], 3)
+    cl, cd = oracle.encrypt_batch(pk, as_bytes(xs), ms, bound)
+    cpu_enc = oracle_leg(lambda: oracle.encrypt_batch(pk, as_bytes(xs), ms, bound), ns, leg_s,
+                         "u32 encryptions (64 values per call)")
+    cpu_dec = oracle_leg(lambda: oracle.decrypt_batch(sk, cl, cd, bound, 32, ns), ns, leg_s,
+                         "u32 decryptions of fresh ciphertexts (64 per call)")
+    cpu_pair = {"value": 1.0 / (1.0 / cpu_enc["value"] + 1.0 / cpu_dec["value"]), "cores": 1,
+                "kind": "port", "cpu": cpu_model(),
+                "sample": "from the encrypt and decrypt legs below (1 thread each)"}
+    # algorithmic bytes per u32 (SURVEY.md s8(d)): encrypt writes 32 x 40 B, reads 32 x 16 B of
+    # masks; decrypt reads the 1280 B and writes 4 B
     out["u32_encrypt_decrypt"] = {
         "value": res["csprng"][0], "unit": "u32 enc+dec/s", "batch": n,
         "verified": res["csprng"][1] and res["predrawn"][1], "steps": reps,
@@ -336,7 +407,55 @@ def secondary_metrics(ctx, device, steps):
         "masks": "drawn per step from the engine CSPRNG (ChaCha20 on device), as the "
                  "reference's getrandom draw is part of its encryption",
         "predrawn_masks": {"value": res["predrawn"][0], "kernel_us_per_step": res["predrawn"][2]},
-        "launch": "one HIP graph replay per step (mask draw + encrypt + decrypt)"}
+        "launch": "one HIP graph replay per step (mask draw + encrypt + decrypt)",
+        "roofline": hbm_roofline(2564 * n, res["predrawn"][2] * 1e-6,
+                                 "encrypt_table_kernel + decrypt_bits_kernel (pre-drawn masks)",
+                                 "2564 algorithmic B per u32 (SURVEY.md s8(d)): 1280 B written by "
+                                 "encrypt, 1280 B read + 4 B written by decrypt; kernel time of "
+                                 "the step by HIP events"),
+        "cpu_baseline": cpu_pair}
+    out["u32_encrypt"] = {
+        "value": encc_r, "unit": "u32 encryptions/s", "batch": n, "kernel_us_per_step": 1e6 * encc_k,
+        "masks": "drawn per step (engine CSPRNG)",
+        "predrawn_masks": {"value": enc_r, "kernel_us_per_step": 1e6 * enc_k},
+        "readme_reference": "76.0 us per u32 on a Ryzen 7 7800X3D, 1 thread (README.md:73)",
+        "roofline": hbm_roofline(1792 * n, enc_k, "encrypt_table_kernel (pre-drawn masks)",
+                                 "1792 algorithmic B per u32: 1280 B of ciphertext written, 512 B "
+                                 "of masks read"),
+        "cpu_baseline": cpu_enc}
+    out["u32_decrypt_fresh"] = {
+        "value": dec_r, "unit": "u32 decryptions/s", "batch": n, "verified": dec_ok,
+        "kernel_us_per_step": 1e6 * dec_k,
+        "readme_reference": "12.5 us per u32 on a Ryzen 7 7800X3D, 1 thread (README.md:74)",
+        "roofline": hbm_roofline(1284 * n, dec_k, "decrypt_bits_kernel",
+                                 "1284 algorithmic B per u32: 1280 B read, 4 B written"),
+        "cpu_baseline": cpu_dec}
+    del c, dec, m
+
+    # README.md:76 "Dec. after add" (benches/u32.rs:47-49): decrypting the 4096 add outputs of
+    # the headline step (46.9 KB of 369-limb polynomials per u32: the rem-heavy case)
+    na = add_out.n
+    dbuf = torch.empty((na, 4), dtype=torch.uint8, device=device)
+    ab = add_out._c()
+    g = ctx.graph(lambda: ctx._launch(lambda: L.hm_decrypt_batch(ctx._h, ctypes.byref(ab),
+                                                                 dbuf.data_ptr()), "decrypt"),
+                  warmup=2)
+    wall, ev_s = time_loop(g.replay, reps, 2, 1)
+    ctx.synchronize()
+    per_u32 = 8 * add_out.stride + 4
+    ol, od = H.value_slice(add_out, 0, 4).to_host()
+    cpu_dadd = oracle_leg(lambda: oracle.decrypt_batch(sk, ol, od, add_out.bound, 32, 4), 4, leg_s,
+                          "u32 decryptions of add outputs (4 per call; long division, "
+                          "polynomial.rs:316-365)")
+    out["u32_decrypt_after_add"] = {
+        "value": na * reps / wall, "unit": "u32 decryptions/s", "batch": na,
+        "kernel_us_per_step": 1e6 * ev_s / reps,
+        "readme_reference": "1.03 ms per u32 on a Ryzen 7 7800X3D, 1 thread (README.md:76)",
+        "roofline": hbm_roofline(per_u32 * na, ev_s / reps, "decrypt_kernel (wave per value)",
+                                 f"{per_u32} algorithmic B per u32: the add output at its static "
+                                 f"capacity read once, 4 B written"),
+        "cpu_baseline": cpu_dadd}
+    del dbuf
 
     # PCIe-inclusive add rate: the same 4096-value add with its inputs copied host->device and
     # its outputs device->host (pinned buffers) inside every step -- what a caller handing host
@@ -364,65 +483,89 @@ def secondary_metrics(ctx, device, steps):
     out["u32_add_pcie_inclusive"] = {"value": n4 * max(4, steps // 2) / wall, "unit": "adds/s",
                                      "batch": n4, "bytes_moved_per_step": moved,
                                      "note": "H2D inputs + add + D2H outputs per step"}
+    del c4a, c4b, o4, host
 
-    # configs[3] feasible form: u8 multiply (carry-save circuit), batch 1024
+    # Multiplies (configs[3]) under an S(0) = 0 key, so that every product's decryption is
+    # checked: u8 multiply, batch 1024, and the low K result bits of the u32 circuit.
+    mctx, mseed = s0_zero_context(device)
     n8 = 1024
     a8 = np.random.default_rng(1).integers(0, 256, size=n8, dtype=np.uint8)
     b8 = np.random.default_rng(2).integers(0, 256, size=n8, dtype=np.uint8)
-    ca, cbb = ctx.encrypt(a8), ctx.encrypt(b8)
-    ob = H.mul_out_bounds(ca.bound, cbb.bound)
-    co = H.Ciphered.empty(n8, ob, device)
-    H.mul_into(ctx, ca, cbb, co)  # sizes the workspace outside the timed loop
-    ctx.synchronize()
-    wall, _ = time_loop(lambda: H.mul_into(ctx, ca, cbb, co), max(1, steps // 4), 1, 1)
-    got = ctx.decrypt(co, np.uint8)
+    ca, cbb = mctx.encrypt(a8), mctx.encrypt(b8)
+    co = H.Ciphered.empty(n8, H.mul_out_bounds(ca.bound, cbb.bound), device)
+    H.mul_into(mctx, ca, cbb, co)  # sizes the workspace outside the timed loop
+    mctx.synchronize()
+    wall, _ = time_loop(lambda: H.mul_into(mctx, ca, cbb, co), max(1, steps // 4), 1, 1)
+    got = mctx.decrypt(co, np.uint8)
     out["u8_mul"] = {"value": n8 * max(1, steps // 4) / wall, "unit": "u8 muls/s", "batch": n8,
-                     "verified": bool(np.array_equal(got, (a8.astype(int) * b8) .astype(np.uint8)))}
+                     "verified": bool(np.array_equal(got, (a8.astype(int) * b8).astype(np.uint8))),
+                     "key_seed": mseed}
+    del ca, cbb, co
 
-    # SURVEY.md §8 row A14, configs[3] (u32 mul, batch 1024): the first MUL_LOW_BENCH result bits
-    # of the u32 carry-save circuit, bit-exact (tests/test_golden.py pins K = 16 to the oracle);
-    # the full u32 circuit is infeasible for any engine and is priced, not run: the planner's own
-    # cost model (hm_mul_cost) scales the measured word-pair rate up to all 32 bits
+    # SURVEY.md s8 row A14, configs[3] (u32 mul, batch 1024): the first K result bits of the u32
+    # carry-save circuit, bit-exact (tests: oracle fixture at K = 16, residue checks of the full
+    # batch at K = 16 and of K = 20); the full u32 circuit is infeasible for any engine and is
+    # priced, not run: the planner's own cost model (hm_mul_cost) scales the measured rate up
     a32 = np.random.default_rng(3).integers(0, 2**32, size=n8, dtype=np.uint32)
     b32 = np.random.default_rng(4).integers(0, 2**32, size=n8, dtype=np.uint32)
-    c32a, c32b = ctx.encrypt(a32), ctx.encrypt(b32)
-    for k in (12, MUL_LOW_BENCH):
+    c32a, c32b = mctx.encrypt(a32), mctx.encrypt(b32)
+    for k, nk in ((12, n8), (MUL_LOW_BENCH, n8), (20, 16)):
         ob = H.mul_out_bounds(c32a.bound[:k], c32b.bound[:k])
-        cp = H.Ciphered.empty(n8, ob, device)
-        H.mul_low_into(ctx, c32a, c32b, k, cp)  # plan + workspace outside the timed loop
-        ctx.synchronize()
-        reps = 2 if k >= 16 else max(2, steps // 4)
-        wall, ev_s = time_loop(lambda: H.mul_low_into(ctx, c32a, c32b, k, cp), reps, 0, 1,
-                               ctx.stream)
-        ctx.synchronize()
-        # decrypt through a 16-bit view: output bits >= k are null polynomials
-        lo16 = ctx.decrypt_bytes(H.pad_bits(cp, 16)).cpu().numpy().view("<u2").reshape(-1)
-        want = ((a32.astype(np.uint64) * b32) & ((1 << k) - 1)).astype(np.uint16)
+        va, vb = H.value_slice(c32a, 0, nk), H.value_slice(c32b, 0, nk)
+        cp = H.Ciphered.empty(nk, ob, device)
+        H.mul_low_into(mctx, va, vb, k, cp)  # plan + workspace outside the timed loop
+        mctx.synchronize()
+        reps = 1 if k >= 20 else 2 if k >= 16 else max(2, steps // 4)
+        wall, ev_s = time_loop(lambda: H.mul_low_into(mctx, va, vb, k, cp), reps, 0, 1,
+                               mctx.stream)
+        mctx.synchronize()
+        # decrypt through a 24-bit view: output bits >= k are null polynomials
+        raw = mctx.decrypt_bytes(H.pad_bits(cp, 24)).cpu().numpy().astype(np.uint64)
+        lo = raw[:, 0] | (raw[:, 1] << np.uint64(8)) | (raw[:, 2] << np.uint64(16))
+        want = (a32[:nk].astype(np.uint64) * b32[:nk]) & np.uint64((1 << k) - 1)
         cost = H.mul_cost(c32a.bound, c32b.bound, k)
-        rate = n8 * reps / wall
+        rate = nk * reps / wall
         out[f"u32_mul_low{k}"] = {
-            "value": rate, "unit": f"u32 muls/s (result bits 0..{k - 1})", "batch": n8,
+            "value": rate, "unit": f"u32 muls/s (result bits 0..{k - 1})", "batch": nk,
             "ms_per_batch": 1e3 * wall / reps, "kernel_ms_per_batch": 1e3 * ev_s / reps,
-            "decrypt_correct": int(np.sum(lo16 == want)), "of": n8,
-            "decrypt_note": "plaintext recovery is the scheme's, not the engine's: with S(0) = 1 "
-                            "(this key) a product's noise of degree >= deg S randomises the "
-                            "decrypted constant term (the reference's own decipher would return "
-                            "the same bits); with S(0) = 0 every product decrypts",
-            "secret_key_s0": int(ctx.get_secret_key().limbs[0] & 1),
+            "decrypt_correct": int(np.sum(lo == want)), "of": nk, "key_seed": mseed,
+            "secret_key_s0": int(mctx.get_secret_key().limbs[0] & 1),
             "word_pairs_per_mul": cost["word_pairs"],
             "word_pairs_per_s": cost["word_pairs"] * rate,
-            "bit_exact": "tests/test_golden.py (K=16 oracle fixture), test_gpu_parity.py"}
+            "bit_exact": "tests/test_golden.py (K=16 oracle fixture, 8 values), "
+                         "test_gpu_properties.py (residue check of all 1024 K=16 products; "
+                         "K=20 Karatsuba = schoolbook + residue check), test_gpu_parity.py"}
         del cp
     full = H.mul_cost(c32a.bound, c32b.bound)
-    k16 = out[f"u32_mul_low{MUL_LOW_BENCH}"]
-    est = k16["word_pairs_per_s"] / full["word_pairs"]
+    kx = out["u32_mul_low20"]
+    est = kx["word_pairs_per_s"] / full["word_pairs"]
     out["u32_mul_full_extrapolated"] = {
         "value": est * 1.0, "unit": "u32 muls/s (EXTRAPOLATED, not measured)",
-        "basis": f"the low-{MUL_LOW_BENCH} rate in word pairs/s (hm_mul_cost) applied to the full "
-                 f"circuit's word pairs; the full circuit also needs its outputs and carries "
-                 f"resident, which no GPU holds",
+        "basis": "the low-20 rate in word pairs/s (hm_mul_cost) applied to the full circuit's "
+                 "word pairs; the full circuit also needs its outputs and carries resident, "
+                 "which no GPU holds",
         "word_pairs_per_mul": full["word_pairs"], "out_bytes_per_mul": full["out_bytes"],
         "max_degree": full["max_degree"], "seconds_per_mul_one_gpu": 1.0 / est}
+    del c32a, c32b, mctx
+    torch.cuda.empty_cache()
+
+    # configs[4]: the mixed workload at its global batch, 2^20 values on this one GPU (the N = 1
+    # point of the strong-scaling configuration), bench.py --workload mixed's own step
+    w = MixedWorkload(1, 0, device, 1 << 20)
+    msteps = 2
+    wall, ev_s = time_loop(w.step, msteps, 1, 1, w.ctx.stream)
+    w.ctx.synchronize()
+    ok_s, ok_p, wall = w.verify(device, wall)
+    out["mixed_config4"] = {
+        "value": w.glob * msteps / wall,
+        "unit": f"u32 values/s (one add + one mul, low {MUL_LOW_K} result bits, per value)",
+        "global_batch": w.glob, "n_gpus": 1, "steps": msteps, "ms_per_step": 1e3 * wall / msteps,
+        "kernel_ms_per_step": 1e3 * ev_s / msteps,
+        "config": {"d": MIXED_PARAMS[0], "dp": MIXED_PARAMS[1], "delta": MIXED_PARAMS[2],
+                   "tau": MIXED_PARAMS[3], "launch_chunk": MIXED_CHUNK},
+        "verified": {"correct_sums": ok_s, "correct_products": ok_p, "of": w.glob}}
+    del w
+    torch.cuda.empty_cache()
     return out
 
 
@@ -515,13 +658,23 @@ def run_add(args, world, rank, device):
                      # as traffic): matrix-core busy cycles and VALU-active cycles over SIMD-cycles
                      **issue,
                      "hbm_gbs_step": n * per_add / kernel_s / 1e9, "alg_bytes_per_add": per_add,
-                     "note": "algorithmic work = schoolbook bit pairs of the chain's carry products "
-                             "P_i * carry_i over the static degree bounds (DESIGN.md s4.1); "
-                             "traffic = PMC HBM bytes of one add step (prep + chain)"},
+                     # the north star's HBM view of the same kernel: algorithmic bytes of the add
+                     # (SURVEY.md s8(d), 49,472 B at d + d' = 256) over the chain's duration
+                     "hbm_achieved_gbs": n * per_add / chain_s / 1e9,
+                     "hbm_frac": n * per_add / chain_s / 1e9 / HBM_PEAK_GBS,
+                     "note": "frac: algorithmic work = schoolbook bit pairs of the chain's carry "
+                             "products P_i * carry_i over the static degree bounds (DESIGN.md "
+                             "s4.1), 2 ops per pair, vs the dense fp4 MFMA peak; hbm_frac: "
+                             "algorithmic bytes per add over the same kernel time vs 8 TB/s; "
+                             "traffic (PMC HBM bytes of one add step, prep + chain), "
+                             "mfma_busy_frac and valu_active_frac are read from "
+                             "profiles/add_traffic.json (rocprofv3 --pmc passes of this bench "
+                             "command), not measured in this run"},
     }
     if rank == 0 and world == 1 and not args.no_secondary:
         try:
-            result["secondary"] = secondary_metrics(ctx, device, max(4, args.steps // 2))
+            result["secondary"] = secondary_metrics(ctx, device, max(4, args.steps // 2), out,
+                                                    args.cpu_seconds)
         except Exception as e:  # reported, never fatal to the headline line
             result["secondary"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu:
