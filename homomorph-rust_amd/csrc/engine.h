@@ -173,14 +173,19 @@ struct MulVProdArgs {
     const MulVTile *tiles;
     uint32_t ntiles;
 };
-// the same leaf products on the matrix cores (mul_mfma.hip): one wave per (value, task), LDS
-// slices of wave_words words (operand images and the output, sized by the launch's largest
-// operands umax, vmax and output omax)
-struct MulLeafArgs {
+// Carry products on the matrix cores (mul_mfma.hip): one wave per (value, task, span of kMfSpan
+// output tiles of 32 words), U in blocks of kMfUB words.  Tasks are the Karatsuba leaves (MulVTask;
+// nspans uniform spans per task) or the column plan's schoolbook products (MulProdTask, with an
+// explicit span list {task, first output word}); vmax = the largest V of the launch (words).
+constexpr int kMfUB = 256;
+constexpr int kMfSpan = 4;
+struct MulMfmaArgs {
     MulBase B;
-    const MulVTask *tasks;
-    uint32_t ntasks;
-    uint32_t umax, vmax, omax, wave_words;
+    const void *tasks;
+    const MulTile *spans; // schoolbook products: {task, base}
+    uint32_t nitems;      // work items per value (leaves: tasks x nspans)
+    uint32_t nspans;      // leaves: spans per task
+    uint32_t vmax, wave_words;
 };
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
 struct KaComb {
@@ -244,8 +249,8 @@ int launch_mul_prod(const MulProdArgs &a, uint32_t w, void *stream);
 int launch_mul_final(const MulFinalArgs &a, void *stream);
 int launch_ka_sum(const KaSumArgs &a, void *stream);
 int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
-int launch_mul_leaf_mfma(const MulLeafArgs &a, void *stream);
-uint32_t mul_leaf_wave_words(uint32_t umax, uint32_t vmax, uint32_t omax);
+int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
+uint32_t mul_mfma_wave_words(uint32_t vmax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);
 int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches

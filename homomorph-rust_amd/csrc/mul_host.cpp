@@ -26,6 +26,9 @@ namespace {
 
 constexpr int64_t kBoundLimit = (int64_t)1 << 30;
 constexpr uint32_t kNW = sizeof(kMulTileW) / sizeof(kMulTileW[0]);
+// schoolbook products whose uniform operand has at least this many words run on the matrix cores
+// (mfma plans); narrower ones keep the VALU tiles
+constexpr uint32_t kMfMinWords = 4;
 
 inline uint32_t slot_words(int64_t bound) { return ((uint32_t)(bound / 32) + 1 + 3) & ~3u; }
 
@@ -53,6 +56,7 @@ struct MulPlan {
     uint32_t L = 0, K = 0;
     bool is_signed = false;
     uint32_t ka_min = 0, ka_leaf = 0;           // Karatsuba options (hm_ctx_set_mul_options)
+    bool mfma = false;                          // products on the matrix cores (hm_ctx_set_mul_products)
     std::vector<uint32_t> ab, bb;
     // geometry
     std::vector<MulSlot> slots;
@@ -66,6 +70,7 @@ struct MulPlan {
         uint32_t maxwords;         // widest prefix / result
         uint32_t prod;             // MulProdTask offset (in tasks)
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
+        uint32_t mspans, nmspans, mvmax;  // MFMA products: MulTile spans (offset / count), max V
         std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
@@ -75,6 +80,7 @@ struct MulPlan {
     std::vector<uint32_t> lists;
     std::vector<MulProdTask> prod;
     std::vector<MulTile> tiles;
+    std::vector<MulTile> mspans; // MFMA spans {task, first output word} of the schoolbook products
     std::vector<KaSum> ka_sums;
     std::vector<MulVTask> ka_vtasks;
     std::vector<MulVTile> ka_vtiles;
@@ -82,6 +88,7 @@ struct MulPlan {
     uint8_t *d_tab = nullptr;
     size_t tab_bytes = 0;
     size_t off_slots = 0, off_pp = 0, off_lists = 0, off_prod = 0, off_tiles = 0, off_res = 0;
+    size_t off_mspans = 0;
     size_t off_ka_sums = 0, off_ka_vtasks = 0, off_ka_vtiles = 0, off_ka_combs = 0;
     uint64_t work = 0; // word-pair products (statistics)
 };
@@ -298,10 +305,19 @@ bool build_plan(MulPlan &P) {
             col.ka.push_back(std::move(pg));
             is_ka[k - col.prod] = true;
         }
-        // tiles of this column's schoolbook products, grouped by per-lane width
+        // tiles of this column's schoolbook products: MFMA spans where the uniform operand has
+        // at least kMfMinWords words (mfma plans), the rest grouped by per-lane VALU tile width
         std::vector<MulTile> byw[kNW];
+        col.mspans = (uint32_t)P.mspans.size(), col.mvmax = 0;
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
             if (is_ka[k - col.prod]) continue;
+            if (P.mfma && P.slots[P.prod[k].u].words >= kMfMinWords) {
+                const uint32_t nout = P.slots[P.prod[k].out].words;
+                for (uint32_t base = 0; base < nout; base += 32 * kMfSpan)
+                    P.mspans.push_back({k - col.prod, base});
+                col.mvmax = std::max(col.mvmax, P.slots[P.prod[k].v].words);
+                continue;
+            }
             const uint32_t nout = P.slots[P.prod[k].out].words;
             const uint32_t need = (nout + 63) / 64;
             uint32_t wc = kNW - 1;
@@ -313,6 +329,7 @@ bool build_plan(MulPlan &P) {
             const uint32_t span = 64 * kMulTileW[wc];
             for (uint32_t base = 0; base < nout; base += span) byw[wc].push_back({k - col.prod, base});
         }
+        col.nmspans = (uint32_t)P.mspans.size() - col.mspans;
         for (uint32_t q = 0; q < kNW; ++q) {
             col.tiles[q] = (uint32_t)P.tiles.size();
             col.ntiles[q] = (uint32_t)byw[q].size();
@@ -351,6 +368,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_prod = o, o = align(o + P.prod.size() * sizeof(MulProdTask));
     P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
+    P.off_mspans = o, o = align(o + P.mspans.size() * sizeof(MulTile));
     P.off_ka_sums = o, o = align(o + P.ka_sums.size() * sizeof(KaSum));
     P.off_ka_vtasks = o, o = align(o + P.ka_vtasks.size() * sizeof(MulVTask));
     P.off_ka_vtiles = o, o = align(o + P.ka_vtiles.size() * sizeof(MulVTile));
@@ -365,6 +383,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_prod, P.prod.data(), P.prod.size() * sizeof(MulProdTask));
     put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
+    put(P.off_mspans, P.mspans.data(), P.mspans.size() * sizeof(MulTile));
     put(P.off_ka_sums, P.ka_sums.data(), P.ka_sums.size() * sizeof(KaSum));
     put(P.off_ka_vtasks, P.ka_vtasks.data(), P.ka_vtasks.size() * sizeof(MulVTask));
     put(P.off_ka_vtiles, P.ka_vtiles.data(), P.ka_vtiles.size() * sizeof(MulVTile));
@@ -383,7 +402,7 @@ hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const 
                    bool is_signed, MulPlan *&out) {
     for (MulPlan *p : c->mul_plans)
         if (p->L == L && p->K == K && p->is_signed == is_signed && p->ka_min == c->ka_min &&
-            p->ka_leaf == c->ka_leaf &&
+            p->ka_leaf == c->ka_leaf && p->mfma == (c->mul_products != HM_MUL_PRODUCTS_VALU) &&
             std::equal(p->ab.begin(), p->ab.end(), ab) && std::equal(p->bb.begin(), p->bb.end(), bb)) {
             out = p;
             return HM_OK;
@@ -391,6 +410,7 @@ hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const 
     auto P = std::make_unique<MulPlan>();
     P->L = L, P->K = K, P->is_signed = is_signed;
     P->ka_min = c->ka_min, P->ka_leaf = c->ka_leaf;
+    P->mfma = c->mul_products != HM_MUL_PRODUCTS_VALU;
     P->ab.assign(ab, ab + K), P->bb.assign(bb, bb + K);
     if (!build_plan(*P)) return HM_ERR_UNSUPPORTED;
     if (hm_status st = upload_plan(c, *P); st) {
@@ -468,11 +488,12 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
     }
     if (c->mul_products != HM_MUL_PRODUCTS_VALU) {
         // the leaves on the matrix cores: one wave per (value, leaf)
-        MulLeafArgs a{};
-        a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask, a.ntasks = pg.nvtask;
-        a.umax = pg.leaf_umax, a.vmax = pg.leaf_vmax, a.omax = pg.leaf_omax;
-        a.wave_words = mul_leaf_wave_words(a.umax, a.vmax, a.omax);
-        if (launch_mul_leaf_mfma(a, c->stream)) return hip_fail(c, hipGetLastError());
+        MulMfmaArgs a{};
+        a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
+        a.nspans = (pg.leaf_omax + 32 * kMfSpan - 1) / (32 * kMfSpan);
+        a.nitems = pg.nvtask * a.nspans;
+        a.vmax = pg.leaf_vmax, a.wave_words = mul_mfma_wave_words(a.vmax);
+        if (launch_mul_mfma(a, true, c->stream)) return hip_fail(c, hipGetLastError());
     } else {
         for (uint32_t q = 0; q < kNW; ++q) {
             if (!pg.ntiles[q]) continue;
@@ -550,6 +571,14 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             sc.out = oa, sc.out_off = ooff[i], sc.out_cap = cap_of(out->bound[i]);
             sc.chunks = (std::max(col.maxwords, 2 * sc.out_cap) + 255) / 256;
             if (launch_mul_scan(sc, c->stream)) return hip_fail(c, hipGetLastError());
+            if (col.nmspans) {
+                MulMfmaArgs mf{};
+                mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_prod) + col.prod;
+                mf.spans = (const MulTile *)(T + P->off_mspans) + col.mspans;
+                mf.nitems = col.nmspans;
+                mf.vmax = col.mvmax, mf.wave_words = mul_mfma_wave_words(mf.vmax);
+                if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
+            }
             for (uint32_t q = 0; q < kNW; ++q) {
                 if (!col.ntiles[q]) continue;
                 MulProdArgs pr{};

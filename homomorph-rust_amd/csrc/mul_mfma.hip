@@ -1,54 +1,64 @@
-// mul_mfma.hip — the multiplier's Karatsuba leaf products (mul_host.cpp "Karatsuba") on the
-// gfx950 matrix cores: out = U * V over GF(2)[X] as a {0,1} Toeplitz GEMM on fp4 MFMA
-// (mfma_gf2.h), replacing mul_vprod_kernel's scalar-decided VALU XORs (mul_engine.hip).
-// Same products as the reference's Polynomial::mul (src/polynomial.rs:252-310): exact, so every
-// bit is identical.
+// mul_mfma.hip — the multiplier's carry products on the gfx950 matrix cores: out = U * V over
+// GF(2)[X] as {0,1} Toeplitz GEMMs on fp4 MFMA (mfma_gf2.h), replacing the scalar-decided VALU
+// XORs of mul_engine.hip (mul_prod_kernel, mul_vprod_kernel).  Same products as the reference's
+// Polynomial::mul (src/polynomial.rs:252-310): exact, so every bit is identical.
 //
-// One wavefront per (value, leaf task).  In its LDS slice the wave builds
-//   RS   the bit-reversed nibble image of U over R = nu + 2 words (+ zero nibbles the last chunk's
-//        window reaches),
-//   VI   the nibble image of V, 16 B per word, with kVHalo zero words below and above,
-//   OUT  the product's words, XOR-accumulated.
-// Chunks (floor(nu/2) + 1 of K = 64) are taken in groups of kLeafG: the group's A fragments
-// (kLeafG x 4 VGPRs) are built once, then every output tile of 32 words that the group reaches is
-// swept, two tiles at a time (independent accumulator chains), each tile one B read per chunk.
-// Each (tile, group) starts its accumulators at 2^23, so its parities are its part of the product
-// mod 2; parts of different groups meet in OUT by XOR (the parity of a sum is the XOR of the
-// parities of its parts).
+// Two kinds of task, one kernel body:
+//   LEAF  the Karatsuba leaves (mul_host.cpp "Karatsuba"): arena views with explicit sizes;
+//   SLOT  the schoolbook carry products p_t * x_t of the column plan: slots whose exact sizes come
+//         from their degree rows (deg1), U = the operand with fewer words.
+// One wavefront per (value, task, output span of kSpan tiles of 32 words).  U is taken in blocks
+// of kUB words (U * V = sum_b X^(32 kUB b) U_b * V).  Per block, in the wave's LDS slice:
+//   RS   the bit-reversed nibble image of U_b over R = ub + 2 words (+ zero nibbles the last
+//        chunk's window reaches),
+//   VI   the nibble image (16 B per word) of the V words the span's windows reach, zero outside V,
+// and across blocks OUT, the span's output words, XOR-accumulated.  Chunks (floor(ub/2) + 1 of
+// K = 64) are taken in groups of G (16, then 4, then 1 for the tail): the group's A fragments are
+// built once, then every tile of the span that the group reaches is swept, two tiles at a time
+// (independent accumulator chains), one B read per chunk and tile.  Each (tile, group) starts its
+// accumulators at 2^23, so its parities are its part of the product mod 2; parts of different
+// groups and blocks meet in OUT by XOR (the parity of a sum is the XOR of the parities of its
+// parts).
 #include <hip/hip_runtime.h>
 
 #include "mfma_gf2.h"
 
 namespace hm {
 
-constexpr int kLeafG = 16;     // chunks per A group (64 VGPRs of A fragments)
-constexpr int kVHalo = 64;     // zero V words below and above the image (>= 2 kLeafG + 32)
-constexpr int kLeafPf = 3;     // B reads issued ahead of their MFMA
+constexpr int kMfG = 16;      // chunks per full A group (64 VGPRs of A fragments)
+constexpr int kMfPf = 3;      // B reads issued ahead of their MFMA
+constexpr int kVPad = 2 * kMfG + 32; // V words read beyond V's ends (zero)
 
-__host__ __device__ constexpr uint32_t leaf_rs_words(uint32_t umax) { return 4 * (umax + 2) + 16; }
-__host__ __device__ constexpr uint32_t leaf_vi_words(uint32_t vmax) { return 4 * (vmax + 2 * kVHalo); }
-__host__ __device__ constexpr uint32_t leaf_wave_words(uint32_t umax, uint32_t vmax, uint32_t omax) {
-    return leaf_rs_words(umax) + leaf_vi_words(vmax) + ((omax + 3) & ~3u);
+__host__ __device__ constexpr uint32_t mf_rs_words() { return 4 * (kMfUB + 2) + 16; }
+// V words one (block, span) reaches: 32 kSpan + 32 + 2 NC (NC <= kMfUB/2 + 1), or all of V plus
+// its zero pads when that is fewer
+__host__ __device__ constexpr uint32_t mf_vi_words(uint32_t vmax) {
+    const uint32_t a = 32 * kMfSpan + 32 + 2 * (kMfUB / 2 + 1), b = vmax + 2 * kVPad;
+    return 4 * ((a < b ? a : b) + 8);
+}
+__host__ __device__ constexpr uint32_t mf_wave_words(uint32_t vmax) {
+    return mf_rs_words() + mf_vi_words(vmax) + 32 * kMfSpan;
 }
 
 __device__ __forceinline__ int floor_div32(int x) { return x >= 0 ? x / 32 : -((31 - x) / 32); }
 
-// Tiles T0 .. T1 (T1 - T0 = 1 or 2) against G chunks from c0: acc per tile, one B read per chunk
-// and tile (window word 32T + col - D + h + 2c of VI), the parities XORed into OUT.
+// Tiles T0 .. T0 + NT - 1 (NT = 1, 2) against G chunks from c0: one accumulator set per tile,
+// one B read per chunk and tile (window word 32T + col - D + h + 2c of VI, whose first word is
+// vlo), the parities XORed into OUT (span-relative tile T - Ts).
 template <int G, int NT>
-__device__ __forceinline__ void leaf_tiles(const v8i (&Af)[G], const uint32_t *VI, int T0, int c0,
-                                           int D, uint32_t *OUT, int nout) {
+__device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI, int vlo, int T0,
+                                         int Ts, int c0, int D, uint32_t *OUT) {
     const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
     const uint4 *bt[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
-        bt[t] = (const uint4 *)VI + (32 * (T0 + t) + col - D + h + 2 * c0 + kVHalo);
+        bt[t] = (const uint4 *)VI + (32 * (T0 + t) + col - D + h + 2 * c0 - vlo);
     v16f acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[t][j] = 8388608.0f;
-    constexpr int P = G < kLeafPf ? G : kLeafPf;
+    constexpr int P = G < kMfPf ? G : kMfPf;
     uint4 bq[NT][G];
 #pragma unroll
     for (int c = 0; c < P; ++c)
@@ -63,22 +73,21 @@ __device__ __forceinline__ void leaf_tiles(const v8i (&Af)[G], const uint32_t *V
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             acc[t] = mfma_fp4(Af[c], b_fragment(bq[t][c]), acc[t]);
-            // keep the reads of later chunks below this MFMA (see adder_mfma.hip tile_mfma)
+            // keep the reads of later chunks below this MFMA (adder_mfma.hip tile_mfma)
             asm volatile("" : "+v"(acc[t])::"memory");
         }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const uint32_t word = join_halves(acc_parities(acc[t]) << (4 * h));
-        const int W = 32 * (T0 + t) + col;
-        if (h == 0 && W < nout) atomicXor(&OUT[W], word); // ds_xor: this wave's words only
+        if (h == 0) atomicXor(&OUT[32 * (T0 + t - Ts) + col], word); // this wave's slice only
     }
 }
 
-// One group of G chunks from c0: A fragments once, then every tile whose window meets V's words
+// One group of G chunks from c0 over the tiles tlo .. thi of the span
 template <int G>
-__device__ __forceinline__ void leaf_group(const uint32_t *RS, const uint32_t *VI, int R, int D, int nv,
-                                           int tiles, int c0, uint32_t *OUT, int nout) {
+__device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
+                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
     const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
     const int jb = 32 * (R - D + h) - 1 - col;
     const uint32_t *rw0 = RS + (jb >> 3) + 8 * c0;
@@ -87,70 +96,101 @@ __device__ __forceinline__ void leaf_group(const uint32_t *RS, const uint32_t *V
 #pragma unroll
     for (int c = 0; c < G; ++c) Af[c] = a_fragment(rw0 + 8 * c, sh);
     // tiles whose windows (words 32T - D + 2c0 .. 32T + 31 - D + 2(c0 + G) - 1) meet [0, nv)
-    const int tlo = max(0, floor_div32(D - 2 * c0 - 2 * G - 30 + 31));
-    const int thi = min(tiles - 1, floor_div32(nv - 1 + D - 2 * c0));
+    const int tlo = max(Ts, floor_div32(D - 2 * c0 - 2 * G + 1));
+    const int thi = min(Te - 1, floor_div32(nv - 1 + D - 2 * c0));
     int T = tlo;
-    for (; T + 1 <= thi; T += 2) leaf_tiles<G, 2>(Af, VI, T, c0, D, OUT, nout);
-    if (T <= thi) leaf_tiles<G, 1>(Af, VI, T, c0, D, OUT, nout);
+    for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT);
+    if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
 }
 
+template <bool LEAF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 3)))
-mul_leaf_mfma_kernel(MulLeafArgs P) {
+mul_mfma_kernel(MulMfmaArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
     nibble_table(tab);
     __syncthreads();
     const int wave = (int)rfl(threadIdx.x >> 6);
     const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    const uint64_t e = g / P.ntasks;
+    const uint64_t e = g / P.nitems;
     if (e >= P.B.nv) return; // whole wave exits together
-    const MulVTask T = P.tasks[g % P.ntasks];
+    const uint32_t item = (uint32_t)(g % P.nitems);
     uint32_t *arena = P.B.arena + e * P.B.astride;
-    uint32_t *O = arena + T.out;
-    const int nu = (int)rfl(T.nu), nv = (int)rfl(T.nv), nout = (int)rfl(T.nout);
+    const uint32_t *U, *V;
+    uint32_t *O;
+    int nu, nv, nout, base;
+    if constexpr (LEAF) {
+        const MulVTask t = ((const MulVTask *)P.tasks)[item / P.nspans];
+        base = (int)(item % P.nspans) * 32 * kMfSpan;
+        U = arena + t.u, V = arena + t.v, O = arena + t.out;
+        nu = (int)rfl(t.nu), nv = (int)rfl(t.nv), nout = (int)rfl(t.nout);
+        if (base >= nout) return;
+    } else {
+        const MulTile tl = P.spans[item];
+        const MulProdTask t = ((const MulProdTask *)P.tasks)[tl.task];
+        base = (int)rfl(tl.base);
+        const uint32_t du = rfl(P.B.deg1[(uint64_t)t.u * P.B.nv + e]);
+        const uint32_t dv = rfl(P.B.deg1[(uint64_t)t.v * P.B.nv + e]);
+        U = arena + P.B.slots[t.u].off, V = arena + P.B.slots[t.v].off;
+        O = arena + P.B.slots[t.out].off;
+        nu = bitwords((int)du), nv = bitwords((int)dv), nout = (int)P.B.slots[t.out].words;
+        if (base == 0 && lane_id() == 0)
+            P.B.deg1[(uint64_t)t.out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+    }
     const int lane = lane_id();
+    const int wend = min(nout, base + 32 * kMfSpan); // this span's output words [base, wend)
     if (nu == 0 || nv == 0) {
-        for (int w = lane; w < nout; w += kWave) O[w] = 0u;
+        for (int w = base + lane; w < wend; w += kWave) O[w] = 0u;
         return;
     }
     uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
-    uint32_t *VI = RS + leaf_rs_words(P.umax);
-    uint32_t *OUT = VI + leaf_vi_words(P.vmax);
-    const uint32_t *U = arena + T.u, *V = arena + T.v;
-    // RS: nibble word k (< 4R) = byte (k & 3) of bitreverse(U[R - 1 - k/4]) as nibbles; zeros after
-    const int R = nu + 2;
-    for (int k = lane; k < (int)leaf_rs_words(P.umax); k += kWave) {
-        const int q = R - 1 - (k >> 2);
-        const uint32_t rev = (k < 4 * R && q < nu) ? __builtin_bitreverse32(U[q]) : 0u;
-        RS[k] = tab[(rev >> (8 * (k & 3))) & 0xFFu];
+    uint32_t *VI = RS + mf_rs_words();
+    uint32_t *OUT = VI + mf_vi_words(P.vmax);
+    for (int w = lane; w < 32 * kMfSpan; w += kWave) OUT[w] = 0u;
+    const int T0 = base >> 5;
+    for (int b0 = 0; b0 < nu; b0 += kMfUB) {
+        // U_b = words [b0, b0 + ub) of U: its product with V lands kb = b0/32 tiles up
+        const int ub = min(kMfUB, nu - b0), kb = b0 >> 5;
+        const int Ts = T0 - kb, Te = Ts + kMfSpan;   // the span in U_b * V's tiles
+        if (Te <= 0) break;                          // this and later blocks land above the span
+        const int D = ub, R = ub + 2, nc = ub / 2 + 1;
+        const int vlo = max(32 * Ts - D, -kVPad);
+        const int vhi = min(32 * Te + 32 - D + 2 * nc, nv + kVPad);
+        wsync(); // the previous block's reads of RS / VI are done
+        for (int k = lane; k < (int)mf_rs_words(); k += kWave) {
+            const int q = R - 1 - (k >> 2);
+            const uint32_t rev = (k < 4 * R && q < ub) ? __builtin_bitreverse32(U[b0 + q]) : 0u;
+            RS[k] = tab[(rev >> (8 * (k & 3))) & 0xFFu];
+        }
+        for (int i = lane; i < vhi - vlo; i += kWave) {
+            const int w = vlo + i;
+            const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
+            uint4 q;
+            q.x = tab[v & 0xFFu], q.y = tab[(v >> 8) & 0xFFu];
+            q.z = tab[(v >> 16) & 0xFFu], q.w = tab[v >> 24];
+            ((uint4 *)VI)[i] = q;
+        }
+        wsync();
+        const int tlo = max(Ts, 0);
+        int c0 = 0;
+        for (; c0 + kMfG <= nc; c0 += kMfG) mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT - 32 * (tlo - Ts));
+        for (; c0 + 4 <= nc; c0 += 4) mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT - 32 * (tlo - Ts));
+        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT - 32 * (tlo - Ts));
     }
-    // VI: word w (-kVHalo <= w < nv + kVHalo) at quad w + kVHalo
-    for (int k = lane; k < 4 * (nv + 2 * kVHalo); k += kWave) {
-        const int w = (k >> 2) - kVHalo;
-        const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
-        VI[k] = tab[(v >> (8 * (k & 3))) & 0xFFu];
-    }
-    for (int w = lane; w < nout; w += kWave) OUT[w] = 0u;
     wsync();
-    const int D = nu, nc = nu / 2 + 1, tiles = (nout + 31) >> 5;
-    int c0 = 0;
-    for (; c0 + kLeafG <= nc; c0 += kLeafG) leaf_group<kLeafG>(RS, VI, R, D, nv, tiles, c0, OUT, nout);
-    for (; c0 < nc; ++c0) leaf_group<1>(RS, VI, R, D, nv, tiles, c0, OUT, nout);
-    wsync();
-    for (int w = lane; w < nout; w += kWave) O[w] = OUT[w];
+    for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
 }
 
-int launch_mul_leaf_mfma(const MulLeafArgs &a, void *stream) {
-    const uint64_t waves = a.B.nv * a.ntasks;
+int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
+    const uint64_t waves = a.B.nv * a.nitems;
     if (!waves) return 0;
     const size_t lds = (256 + (size_t)a.wave_words * 4) * 4;
-    hipLaunchKernelGGL(mul_leaf_mfma_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
-                       (hipStream_t)stream, a);
+    const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+    if (leaf) hipLaunchKernelGGL(mul_mfma_kernel<true>, grid, block, lds, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(mul_mfma_kernel<false>, grid, block, lds, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-uint32_t mul_leaf_wave_words(uint32_t umax, uint32_t vmax, uint32_t omax) {
-    return leaf_wave_words(umax, vmax, omax);
-}
+uint32_t mul_mfma_wave_words(uint32_t vmax) { return mf_wave_words(vmax); }
 
 } // namespace hm
