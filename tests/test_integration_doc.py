@@ -21,7 +21,8 @@ STD = {
     "iter", "map", "collect", "max", "min", "unwrap_or", "unwrap_or_else", "len", "as_ptr",
     "as_mut_ptr", "cast", "enumerate", "take", "clone", "first", "map_or", "into_iter", "pop",
     "ok", "lock", "unwrap", "as_ref", "push", "with_capacity", "into_boxed_slice", "var_os", "var",
-    "into", "null_mut", "null", "is_some", "new", "from", "fmt", "main",
+    "into", "null_mut", "null", "is_some", "new", "from", "fmt", "main", "borrow_mut", "get_mut",
+    "into_inner", "is_null", "iter_mut",
 }
 
 
