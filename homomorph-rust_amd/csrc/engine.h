@@ -173,18 +173,20 @@ struct MulVProdArgs {
     const MulVTile *tiles;
     uint32_t ntiles;
 };
-// Carry products on the matrix cores (mul_mfma.hip): one wave per (value, task, span of kMfSpan
-// output tiles of 32 words), U in blocks of kMfUB words.  Tasks are the Karatsuba leaves (MulVTask;
+// Carry products on the matrix cores (mul_mfma.hip): one wave per (value, task, span of `span`
+// output tiles of 32 words; a leaf's whole output, kMfSpan tiles of a schoolbook product), U in
+// blocks of kMfUB words.  Tasks are the Karatsuba leaves (MulVTask;
 // nspans uniform spans per task) or the column plan's schoolbook products (MulProdTask, with an
 // explicit span list {task, first output word}); vmax = the largest V of the launch (words).
 constexpr int kMfUB = 256;
-constexpr int kMfSpan = 4;
+constexpr int kMfSpan = 16;
 struct MulMfmaArgs {
     MulBase B;
     const void *tasks;
     const MulTile *spans; // schoolbook products: {task, base}
     uint32_t nitems;      // work items per value (leaves: tasks x nspans)
     uint32_t nspans;      // leaves: spans per task
+    uint32_t span;        // output tiles per span
     uint32_t vmax, wave_words;
 };
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
@@ -250,7 +252,7 @@ int launch_mul_final(const MulFinalArgs &a, void *stream);
 int launch_ka_sum(const KaSumArgs &a, void *stream);
 int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
-uint32_t mul_mfma_wave_words(uint32_t vmax);
+uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span);
 int launch_ka_comb(const KaCombArgs &a, void *stream);
 int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches

@@ -490,9 +490,10 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         // the leaves on the matrix cores: one wave per (value, leaf)
         MulMfmaArgs a{};
         a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
-        a.nspans = (pg.leaf_omax + 32 * kMfSpan - 1) / (32 * kMfSpan);
-        a.nitems = pg.nvtask * a.nspans;
-        a.vmax = pg.leaf_vmax, a.wave_words = mul_mfma_wave_words(a.vmax);
+        a.span = std::max(1u, (pg.leaf_omax + 31) / 32); // one span: the whole leaf output
+        a.nspans = 1;
+        a.nitems = pg.nvtask;
+        a.vmax = pg.leaf_vmax, a.wave_words = mul_mfma_wave_words(a.vmax, a.span);
         if (launch_mul_mfma(a, true, c->stream)) return hip_fail(c, hipGetLastError());
     } else {
         for (uint32_t q = 0; q < kNW; ++q) {
@@ -575,8 +576,8 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 MulMfmaArgs mf{};
                 mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_prod) + col.prod;
                 mf.spans = (const MulTile *)(T + P->off_mspans) + col.mspans;
-                mf.nitems = col.nmspans;
-                mf.vmax = col.mvmax, mf.wave_words = mul_mfma_wave_words(mf.vmax);
+                mf.nitems = col.nmspans, mf.span = kMfSpan;
+                mf.vmax = col.mvmax, mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span);
                 if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
             }
             for (uint32_t q = 0; q < kNW; ++q) {

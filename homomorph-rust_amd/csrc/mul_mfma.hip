@@ -7,7 +7,7 @@
 //   LEAF  the Karatsuba leaves (mul_host.cpp "Karatsuba"): arena views with explicit sizes;
 //   SLOT  the schoolbook carry products p_t * x_t of the column plan: slots whose exact sizes come
 //         from their degree rows (deg1), U = the operand with fewer words.
-// One wavefront per (value, task, output span of kSpan tiles of 32 words).  U is taken in blocks
+// One wavefront per (value, task, output span of `span` tiles of 32 words).  U is taken in blocks
 // of kUB words (U * V = sum_b X^(32 kUB b) U_b * V).  Per block, in the wave's LDS slice:
 //   RS   the bit-reversed nibble image of U_b over R = ub + 2 words (+ zero nibbles the last
 //        chunk's window reaches),
@@ -30,14 +30,14 @@ constexpr int kMfPf = 3;      // B reads issued ahead of their MFMA
 constexpr int kVPad = 2 * kMfG + 32; // V words read beyond V's ends (zero)
 
 __host__ __device__ constexpr uint32_t mf_rs_words() { return 4 * (kMfUB + 2) + 16; }
-// V words one (block, span) reaches: 32 kSpan + 32 + 2 NC (NC <= kMfUB/2 + 1), or all of V plus
+// V words one (block, span) reaches: 32 span + 32 + 2 NC (NC <= kMfUB/2 + 1), or all of V plus
 // its zero pads when that is fewer
-__host__ __device__ constexpr uint32_t mf_vi_words(uint32_t vmax) {
-    const uint32_t a = 32 * kMfSpan + 32 + 2 * (kMfUB / 2 + 1), b = vmax + 2 * kVPad;
+__host__ __device__ constexpr uint32_t mf_vi_words(uint32_t vmax, uint32_t span) {
+    const uint32_t a = 32 * span + 32 + 2 * (kMfUB / 2 + 1), b = vmax + 2 * kVPad;
     return 4 * ((a < b ? a : b) + 8);
 }
-__host__ __device__ constexpr uint32_t mf_wave_words(uint32_t vmax) {
-    return mf_rs_words() + mf_vi_words(vmax) + 32 * kMfSpan;
+__host__ __device__ constexpr uint32_t mf_wave_words(uint32_t vmax, uint32_t span) {
+    return mf_rs_words() + mf_vi_words(vmax, span) + 32 * span;
 }
 
 __device__ __forceinline__ int floor_div32(int x) { return x >= 0 ? x / 32 : -((31 - x) / 32); }
@@ -121,7 +121,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
     int nu, nv, nout, base;
     if constexpr (LEAF) {
         const MulVTask t = ((const MulVTask *)P.tasks)[item / P.nspans];
-        base = (int)(item % P.nspans) * 32 * kMfSpan;
+        base = (int)(item % P.nspans) * 32 * (int)P.span;
         U = arena + t.u, V = arena + t.v, O = arena + t.out;
         nu = (int)rfl(t.nu), nv = (int)rfl(t.nv), nout = (int)rfl(t.nout);
         if (base >= nout) return;
@@ -138,20 +138,21 @@ mul_mfma_kernel(MulMfmaArgs P) {
             P.B.deg1[(uint64_t)t.out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
     }
     const int lane = lane_id();
-    const int wend = min(nout, base + 32 * kMfSpan); // this span's output words [base, wend)
+    const int span = (int)P.span;
+    const int wend = min(nout, base + 32 * span); // this span's output words [base, wend)
     if (nu == 0 || nv == 0) {
         for (int w = base + lane; w < wend; w += kWave) O[w] = 0u;
         return;
     }
     uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
     uint32_t *VI = RS + mf_rs_words();
-    uint32_t *OUT = VI + mf_vi_words(P.vmax);
-    for (int w = lane; w < 32 * kMfSpan; w += kWave) OUT[w] = 0u;
+    uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span);
+    for (int w = lane; w < 32 * span; w += kWave) OUT[w] = 0u;
     const int T0 = base >> 5;
     for (int b0 = 0; b0 < nu; b0 += kMfUB) {
         // U_b = words [b0, b0 + ub) of U: its product with V lands kb = b0/32 tiles up
         const int ub = min(kMfUB, nu - b0), kb = b0 >> 5;
-        const int Ts = T0 - kb, Te = Ts + kMfSpan;   // the span in U_b * V's tiles
+        const int Ts = T0 - kb, Te = Ts + span;      // the span in U_b * V's tiles
         if (Te <= 0) break;                          // this and later blocks land above the span
         const int D = ub, R = ub + 2, nc = ub / 2 + 1;
         const int vlo = max(32 * Ts - D, -kVPad);
@@ -173,9 +174,9 @@ mul_mfma_kernel(MulMfmaArgs P) {
         wsync();
         const int tlo = max(Ts, 0);
         int c0 = 0;
-        for (; c0 + kMfG <= nc; c0 += kMfG) mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT - 32 * (tlo - Ts));
-        for (; c0 + 4 <= nc; c0 += 4) mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT - 32 * (tlo - Ts));
-        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT - 32 * (tlo - Ts));
+        for (; c0 + kMfG <= nc; c0 += kMfG) mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT + 32 * (tlo - Ts));
+        for (; c0 + 4 <= nc; c0 += 4) mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT + 32 * (tlo - Ts));
+        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT + 32 * (tlo - Ts));
     }
     wsync();
     for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
@@ -191,6 +192,6 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-uint32_t mul_mfma_wave_words(uint32_t vmax) { return mf_wave_words(vmax); }
+uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span) { return mf_wave_words(vmax, span); }
 
 } // namespace hm
