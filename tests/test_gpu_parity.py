@@ -489,3 +489,50 @@ def test_add_output_capacity_is_checked(H, chain):
     with pytest.raises(H.EngineError):
         H.add_into(ctx, ca, cb, out)
         ctx.synchronize()
+
+
+def _u128(rng, n):
+    """n random u128 plaintexts as Python ints and as their bincode fixint LE images (n, 16)."""
+    vals = [int.from_bytes(rng.bytes(16), "little") for _ in range(n)]
+    img = np.frombuffer(b"".join(v.to_bytes(16, "little") for v in vals), dtype=np.uint8)
+    return vals, img.reshape(n, 16).copy()
+
+
+@pytest.mark.parametrize("op", ["add", "and", "or", "xor", "not"])
+def test_u128_parity(H, oracle, op):
+    """u128, the widest type the reference implements (uint.rs:58, 77): add and the gates on
+    128-bit ciphertexts, bit-exact vs the oracle, plaintexts as (n, 16) byte images."""
+    params = (64, 16, 1, 16)
+    d, dp, delta, tau = params
+    # a key with S(0) = 0: every output decrypts to the plaintext result whatever its noise
+    seed = next(s for s in range(128, 1000) if not int(keys(*params, s)[0][0]) & 1)
+    ctx = make_ctx(H, params, seed)
+    sk, pk, _ = keys(*params, seed)
+    n = 4
+    rng = np.random.default_rng(129)
+    av, ai = _u128(rng, n)
+    bv, bi = _u128(rng, n)
+    ma, mb = masks(n, 128, tau, 130), masks(n, 128, tau, 131)
+    ca, cb = ctx.encrypt(ai, masks=ma), ctx.encrypt(bi, masks=mb)
+    opcls = {"add": H.HomomorphicAddition, "and": H.HomomorphicAndGate, "or": H.HomomorphicOrGate,
+             "xor": H.HomomorphicXorGate, "not": H.HomomorphicNotGate}[op]
+    co = ctx.apply1(opcls, ca) if op == "not" else ctx.apply2(opcls, ca, cb)
+    dec = ctx.decrypt_bytes(co).cpu().numpy()
+    ctx.synchronize()
+    bound = fresh_bound(d, dp, 128)
+    la, da = oracle.encrypt_batch(pk, ai, ma, bound)
+    lb, db = oracle.encrypt_batch(pk, bi, mb, bound)
+    if op == "add":
+        rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, 128, n, co.bound)
+    else:
+        rl, rd = oracle.gate_batch(op, la, da, bound, lb, db, bound, 128, n, co.bound)
+    gl, gd = co.to_host()
+    assert_batches_equal(gl, gd, rl, rd, co.bound, n, f"u128 {op}")
+    rdec = oracle.decrypt_batch(sk, rl, rd, co.bound, 128, n)
+    assert np.array_equal(dec, rdec)
+    M = (1 << 128) - 1
+    f = {"add": lambda x, y: (x + y) & M, "and": lambda x, y: x & y, "or": lambda x, y: x | y,
+         "xor": lambda x, y: x ^ y, "not": lambda x, y: ~x & M}[op]
+    want = [f(x, y) for x, y in zip(av, bv)]
+    got = [int.from_bytes(bytes(r), "little") for r in dec]
+    assert got == want
