@@ -158,11 +158,15 @@ mul_mfma_kernel(MulMfmaArgs P) {
         const int vlo = max(32 * Ts - D, -kVPad);
         const int vhi = min(32 * Te + 32 - D + 2 * nc, nv + kVPad);
         wsync(); // the previous block's reads of RS / VI are done
-        for (int k = lane; k < (int)mf_rs_words(); k += kWave) {
-            const int q = R - 1 - (k >> 2);
-            const uint32_t rev = (k < 4 * R && q < ub) ? __builtin_bitreverse32(U[b0 + q]) : 0u;
-            RS[k] = tab[(rev >> (8 * (k & 3))) & 0xFFu];
+        // RS quad R-1-q = the nibbles of bitreverse(U_b[q]) (one load, one 16-B store per word)
+        for (int q = lane; q < R; q += kWave) {
+            const uint32_t rev = q < ub ? __builtin_bitreverse32(U[b0 + q]) : 0u;
+            uint4 x;
+            x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
+            x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
+            ((uint4 *)RS)[R - 1 - q] = x;
         }
+        for (int k = 4 * R + lane; k < (int)mf_rs_words(); k += kWave) RS[k] = 0u;
         for (int i = lane; i < vhi - vlo; i += kWave) {
             const int w = vlo + i;
             const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
@@ -173,10 +177,17 @@ mul_mfma_kernel(MulMfmaArgs P) {
         }
         wsync();
         const int tlo = max(Ts, 0);
+        uint32_t *OUTs = OUT + 32 * (tlo - Ts);
+        // groups of 16 chunks; a block of 2 mod 32 words (nc = 1 mod 16, e.g. the 129 chunks of a
+        // 256-word leaf) folds its odd chunk into the last group instead of a 1-chunk pass (whose
+        // parity gathers would cost as much as its MFMAs)
+        const bool fold = nc % kMfG == 1 && nc > kMfG;
         int c0 = 0;
-        for (; c0 + kMfG <= nc; c0 += kMfG) mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT + 32 * (tlo - Ts));
-        for (; c0 + 4 <= nc; c0 += 4) mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT + 32 * (tlo - Ts));
-        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUT + 32 * (tlo - Ts));
+        for (; c0 + kMfG + (fold ? 1 : 0) < nc + (fold ? 0 : 1); c0 += kMfG)
+            mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        if (fold) mf_group<kMfG + 1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += kMfG + 1;
+        for (; c0 + 4 <= nc; c0 += 4) mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
     }
     wsync();
     for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
