@@ -572,6 +572,7 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
 MIXED_PARAMS = (256, 256, 1, 256)  # BASELINE.json configs[4]: d = dp = tau = 256, delta = 1
 MIXED_CHUNK = 131072                # values per launch (the 8-GPU shard of 2^20)
 MUL_LOW_K = 8                       # result bits of the multiply half
+MIXED_KARATSUBA = (192, 192)        # hm_ctx_set_mul_options for the multiply half
 
 
 def run_add(args, world, rank, device):
@@ -695,6 +696,10 @@ class MixedWorkload:
             raise SystemExit("--batch must divide by the number of ranks")
         self.world, self.rank, self.glob = world, rank, glob
         self.ctx = ctx = make_context(world, rank, device, MIXED_PARAMS)
+        # Karatsuba leaves of at most 192 words for products from 192 words up: the fastest
+        # strategy for this workload's multiply (scripts/mul_rate.py sweep);
+        # every strategy gives identical bits
+        ctx.set_mul_options(*MIXED_KARATSUBA)
         self.n = n = glob // world
         self.a, self.b = shard_inputs(rank, n)
         self.ca, self.cb = ctx.encrypt(self.a), ctx.encrypt(self.b)  # seeded engine CSPRNG masks

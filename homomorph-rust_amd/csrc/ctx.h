@@ -63,7 +63,7 @@ struct hm_ctx {
     std::vector<hm::MulPlan *> mul_plans; // owned; freed by mul_plans_release
     // Karatsuba carry products (hm_ctx_set_mul_options): shorter operand >= ka_min words (0 =
     // never), recursion down to leaves of at most ka_leaf words
-    uint32_t ka_min = 1024, ka_leaf = 256;
+    uint32_t ka_min = 256, ka_leaf = 256;
     // where the Karatsuba leaf products run (hm_ctx_set_mul_products): HM_MUL_PRODUCTS_*
     uint32_t mul_products = 0;
     // carry chain of the adder (hm_ctx_set_add_options): HM_ADD_CHAIN_AUTO / _MFMA / _VALU

@@ -451,7 +451,7 @@ class Context:
                "hm_ctx_kernel_timing")
         return t.value, n.value
 
-    def set_mul_options(self, karatsuba_min_words: int = 1024, karatsuba_leaf_words: int = 256):
+    def set_mul_options(self, karatsuba_min_words: int = 256, karatsuba_leaf_words: int = 256):
         """hm_ctx_set_mul_options: which carry products of the multiplier run as Karatsuba
         recursions (shorter operand >= karatsuba_min_words words; 0 = never) and their leaf
         size.  Results are identical either way (every product is exact)."""

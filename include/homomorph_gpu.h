@@ -152,7 +152,8 @@ hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
  * carry-save circuit whose shorter operand has at least karatsuba_min_words 32-bit words runs as
  * a Karatsuba recursion down to leaves of at most karatsuba_leaf_words
  * words (rounded to a multiple of 32, at most 512); smaller products run as schoolbook tiles.
- * karatsuba_min_words = 0 disables it.  Defaults: 1024 and 256. */
+ * karatsuba_min_words = 0 disables it.  Defaults: 256 and 256 (measured best for the u32 multiply
+ * prefixes at d = d' = 128 once the leaves run on the matrix cores; 192 and 192 at d = d' = 256). */
 hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
                                  uint32_t karatsuba_leaf_words);
 
