@@ -285,16 +285,29 @@ __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
     }
 }
 
+int launch_add_prep(const AddArgs &a, void *stream) {
+    if (a.n == 0) return 0;
+    // wpv waves per value, 4 waves per block
+    const uint64_t waves = a.n * a.wpv;
+    const uint64_t blocks = (waves + 3) / 4;
+    hipLaunchKernelGGL(add_prep_kernel, dim3((unsigned)blocks), dim3(256),
+                       (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n) {
+    AddArgs s = a;
+    s.a.limbs += e0 * a.a.stride, s.a.degree += e0 * a.a.dstride;
+    s.b.limbs += e0 * a.b.stride, s.b.degree += e0 * a.b.dstride;
+    s.out.limbs += e0 * a.out.stride, s.out.degree += e0 * a.out.dstride;
+    s.ws += e0 * a.ws_stride;
+    s.n = n;
+    return s;
+}
+
 int launch_add(const AddArgs &a, void *stream, void *ev0, void *ev1) {
     if (a.n == 0) return 0;
-    // prep: wpv waves per value, 4 waves per block
-    {
-        const uint64_t waves = a.n * a.wpv;
-        const uint64_t blocks = (waves + 3) / 4;
-        hipLaunchKernelGGL(add_prep_kernel, dim3((unsigned)blocks), dim3(256),
-                           (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
-        if (hipGetLastError() != hipSuccess) return -1;
-    }
+    if (launch_add_prep(a, stream)) return -1;
     if (ev0 && hipEventRecord((hipEvent_t)ev0, (hipStream_t)stream) != hipSuccess) return -1;
     int rc = 0;
     if (a.mfma) rc = launch_add_chain_mfma(a, stream);

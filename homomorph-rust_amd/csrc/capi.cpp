@@ -269,6 +269,9 @@ void hm_ctx_destroy(hm_ctx *c) {
         if (p) (void)hipFree(p);
     for (auto &r : c->retired) (void)hipFree(r.p);
     for (auto &e : c->tev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_fork, c->ev_mid, c->ev_join})
+        if (e) (void)hipEventDestroy(e);
+    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     wipe(c->chacha_key, sizeof(c->chacha_key));
     wipe(&c->rng, sizeof(c->rng));
@@ -448,6 +451,12 @@ hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) {
     if (!c || (ka_min && (ka_leaf < 32 || ka_leaf > 512))) return HM_ERR_INVALID_ARGUMENT;
     c->ka_min = ka_min;
     c->ka_leaf = ka_leaf & ~31u;
+    return HM_OK;
+}
+
+hm_status hm_ctx_set_add_pipeline(hm_ctx *c, int enable) {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    c->add_pipe = enable != 0;
     return HM_OK;
 }
 
@@ -731,6 +740,31 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
             ev[0] = c->tev[c->tev_used], ev[1] = c->tev[c->tev_used + 1];
             c->tev_used += 2;
         }
+    }
+    // Two-stage pipeline (not while timing the chain): the batch in two halves, the second
+    // half's prep on the auxiliary stream right after the first half's, so it runs beside the
+    // first half's chain (the chain is matrix-core and latency bound, the prep VALU bound); the
+    // halves use disjoint workspace and outputs.  Fork / join by events, so a graph captured on
+    // the context stream holds both branches.
+    if (c->add_pipe && !c->time_chain && A.mfma && a->n >= 2 * kAddPipeMin) {
+        if (!c->aux_stream) {
+            HM_HIP(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+            for (hipEvent_t *e : {&c->ev_fork, &c->ev_mid, &c->ev_join})
+                HM_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+        }
+        const uint64_t h = (a->n / 2 + kAddWavesPerBlock - 1) / kAddWavesPerBlock * kAddWavesPerBlock;
+        const AddArgs A1 = add_args_slice(A, 0, h), A2 = add_args_slice(A, h, a->n - h);
+        HM_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+        HM_HIP(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+        if (launch_add_prep(A1, c->stream)) return hip_fail(c, hipGetLastError());
+        HM_HIP(c, hipEventRecord(c->ev_mid, c->stream));
+        if (launch_add_chain_mfma(A1, c->stream)) return hip_fail(c, hipGetLastError());
+        HM_HIP(c, hipStreamWaitEvent(c->aux_stream, c->ev_mid, 0));
+        if (launch_add_prep(A2, c->aux_stream)) return hip_fail(c, hipGetLastError());
+        if (launch_add_chain_mfma(A2, c->aux_stream)) return hip_fail(c, hipGetLastError());
+        HM_HIP(c, hipEventRecord(c->ev_join, c->aux_stream));
+        HM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        return HM_OK;
     }
     return launch_add(A, c->stream, ev[0], ev[1]) ? hip_fail(c, hipGetLastError()) : HM_OK;
 }

@@ -68,6 +68,12 @@ struct hm_ctx {
     uint32_t mul_products = 0;
     // carry chain of the adder (hm_ctx_set_add_options): HM_ADD_CHAIN_AUTO / _MFMA / _VALU
     uint32_t add_chain = 0;
+    // adder pipelining (hm_ctx_set_add_pipeline, off by default): batches of at least
+    // 2 * kAddPipeMin values run as two halves, the second half's prep on aux_stream beside the
+    // first half's chain
+    bool add_pipe = false;
+    hipStream_t aux_stream = nullptr;  // created on first use
+    hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
     // per-launch timing of the adder's carry-chain kernel (hm_ctx_set_kernel_timing): a pair of
     // HIP events recorded around each chain launch on the engine stream
     bool time_chain = false;

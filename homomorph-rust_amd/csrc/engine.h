@@ -239,6 +239,9 @@ struct RandArgs {
 int launch_random(const RandArgs &a, void *stream);
 // ev0/ev1 (hipEvent_t, may be null): recorded on the stream around the carry-chain launch
 int launch_add(const AddArgs &a, void *stream, void *ev0 = nullptr, void *ev1 = nullptr);
+int launch_add_prep(const AddArgs &a, void *stream);
+// the same add over values [e0, e0 + n) of a batch: argument block with every pointer advanced
+AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n);
 int launch_add_chain_mfma(const AddArgs &a, void *stream);
 int launch_add_chain_valu(const AddArgs &a, void *stream);
 int launch_encrypt(const EncArgs &a, void *stream);
@@ -261,6 +264,7 @@ int launch_poly_mul(const PolyArgs &a, void *stream);
 int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
+constexpr uint64_t kAddPipeMin = 1024; // values per half of a pipelined add (hm_ctx_set_add_pipeline)
 constexpr size_t kTimedLaunches = 4096; // chain launches hm_ctx_set_kernel_timing can record
 // MFMA carry chain (adder_mfma.hip), one configuration per chunk count NC: P_i within 2 NC - 1
 // words (NC = 13: 25 words, d + d' <= 256; NC = 25: 49 words, d + d' <= 512), nibble ring slots

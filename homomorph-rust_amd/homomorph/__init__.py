@@ -438,6 +438,12 @@ class Context:
         _check(lib().hm_ctx_set_add_options(self._h, self.ADD_CHAINS[chain]),
                "hm_ctx_set_add_options")
 
+    def set_add_pipeline(self, enable: bool = True):
+        """hm_ctx_set_add_pipeline: run big MFMA-chain adds as two halves whose second prep
+        overlaps the first chain (default off: no faster on configs[1]).  Results are identical
+        either way."""
+        _check(lib().hm_ctx_set_add_pipeline(self._h, int(bool(enable))), "hm_ctx_set_add_pipeline")
+
     def set_kernel_timing(self, enable: bool = True):
         """hm_ctx_set_kernel_timing: record HIP events around every carry-chain launch of the
         adder (outside graph capture) from now on; kernel_timing() reads them back."""

@@ -175,6 +175,13 @@ hm_status hm_ctx_set_mul_products(hm_ctx *ctx, uint32_t products);
 #define HM_ADD_CHAIN_VALU 2u
 hm_status hm_ctx_set_add_options(hm_ctx *ctx, uint32_t chain);
 
+/* Adder pipelining (no effect on results; off by default: measured no faster on configs[1],
+ * DESIGN.md s4.1).  When enabled, an MFMA-chain add of at least 2048 values runs as two halves,
+ * the second half's carry-independent prep on an auxiliary stream beside the first half's carry
+ * chain, joined back into the context stream by events (a graph captured on the context stream
+ * holds both branches).  Not used while kernel timing is on. */
+hm_status hm_ctx_set_add_pipeline(hm_ctx *ctx, int enable);
+
 /* Kernel timing (measurement only; no effect on results).  While enabled, every hm_add_batch
  * outside a stream capture records a pair of HIP events on the engine stream around its
  * carry-chain kernel (the dominant kernel of the add), up to 4096 launches; enabling resets the

@@ -261,6 +261,23 @@ def test_add_skewed_bounds(H, oracle, chain, skew):
     assert np.array_equal(dec, rdec)
 
 
+def test_add_pipeline_same_bits(H):
+    """hm_ctx_set_add_pipeline: a 2048-value add as two stream-pipelined halves writes the same
+    ciphertexts as the one-pass add (the halves use disjoint workspace and outputs)."""
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 77)
+    n = 2048
+    ca = ctx.encrypt(plain(n, np.uint32, 78))
+    cb = ctx.encrypt(plain(n, np.uint32, 79))
+    one = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    ctx.set_add_pipeline(True)
+    two = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    ctx.synchronize()
+    l1, d1 = one.to_host()
+    l2, d2 = two.to_host()
+    assert_batches_equal(l1, d1, l2, d2, one.bound, n, "pipelined add")
+
+
 def test_add_chain_mfma_unsupported(H):
     """A forced MFMA chain on a plan whose P_i exceeds 49 words (d + dp = 1024: 97 words) is
     refused, not approximated."""
