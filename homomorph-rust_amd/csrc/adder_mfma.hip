@@ -137,7 +137,6 @@ add_chain_mfma_kernel(AddArgs A) {
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     if (e >= A.n) return; // whole wave exits together
     const int lane = lane_id();
-    const int col = lane & 31, h = lane >> 5;
     const uint32_t L = A.nbits;
     // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][RS: kRsWords]
     uint32_t *Ls = lds + 256 + (size_t)wave * A.chain_lds;

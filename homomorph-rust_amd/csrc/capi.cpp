@@ -870,16 +870,32 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
     if (!nz) return HM_ERR_DIVIDE_BY_ZERO;           // polynomial.rs:319-322
     const size_t ds = degree_of(s, sn);
     if (ds == 0) return HM_ERR_DIVISOR_IS_ONE;       // the reference never terminates
-    const size_t sl = ds / 64 + 1;
+    if (a->cap > 512) return HM_ERR_UNSUPPORTED;     // poly_rem_kernel: 8 limbs per lane
+    // remainder table: row j, bit k = bit j of X^k mod S, for k < 64 * a->cap
+    const size_t sl = ds / 64 + 1, acap = a->cap;
+    std::vector<uint64_t> zt(ds * acap, 0), r(sl, 0);
+    r[0] = 1; // X^0 mod S (deg S >= 1)
+    for (size_t k = 0; k < 64 * acap; ++k) {
+        for (size_t j = 0; j < ds; ++j)
+            if ((r[j / 64] >> (j % 64)) & 1) zt[j * acap + k / 64] |= 1ull << (k % 64);
+        uint64_t carry = 0; // r = X * r mod S
+        for (size_t w = 0; w < sl; ++w) {
+            const uint64_t nc = r[w] >> 63;
+            r[w] = (r[w] << 1) | carry;
+            carry = nc;
+        }
+        if ((r[ds / 64] >> (ds % 64)) & 1)
+            for (size_t w = 0; w < sl; ++w) r[w] ^= s[w];
+    }
     DeviceGuard g(c->device);
     size_t have = c->d_s_limbs * 8;
-    HM_HIP(c, grow(c, c->d_s, have, sl * 8));
+    HM_HIP(c, grow(c, c->d_s, have, zt.size() * 8));
     c->d_s_limbs = have / 8;
-    HM_HIP(c, hipMemcpyAsync(c->d_s, s, sl * 8, hipMemcpyHostToDevice, c->stream));
-    HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer may be released after return
-    return launch_poly_rem(poly_args(c, a, nullptr, out), c->d_s, (uint32_t)ds, c->stream)
-               ? hip_fail(c, hipGetLastError())
-               : HM_OK;
+    HM_HIP(c, hipMemcpyAsync(c->d_s, zt.data(), zt.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer is released after return
+    const int rc = launch_poly_rem(poly_args(c, a, nullptr, out), c->d_s, (uint32_t)ds, c->stream);
+    if (rc == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
+    return rc ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 
 hm_status hm_ctx_synchronize(hm_ctx *c) {

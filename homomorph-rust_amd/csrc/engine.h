@@ -261,7 +261,8 @@ int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches
 int launch_poly_add(const PolyArgs &a, void *stream);
 int launch_poly_mul(const PolyArgs &a, void *stream);
-int launch_poly_rem(const PolyArgs &a, const uint64_t *s, uint32_t s_deg, void *stream);
+// zt: the remainder table (kernels.hip poly_rem_kernel), s_deg rows of a.acap limbs
+int launch_poly_rem(const PolyArgs &a, const uint64_t *zt, uint32_t s_deg, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
 constexpr uint64_t kAddPipeMin = 1024; // values per half of a pipelined add (hm_ctx_set_add_pipeline)

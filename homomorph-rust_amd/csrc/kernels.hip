@@ -108,33 +108,49 @@ __global__ void __launch_bounds__(256) poly_mul_kernel(PolyArgs P) {
     zero_tail_and_degree(o, P.ocap, deg, P.odeg + e, nout);
 }
 
-// Remainder by one divisor S: thread per polynomial, bitwise long division in place on the output
-// (polynomial.rs:316-365: XOR S << (r_deg - deg S) while r_deg >= deg S).
-__global__ void __launch_bounds__(256) poly_rem_kernel(PolyArgs P, const uint64_t *S, uint32_t sdeg) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Remainder by one divisor S (polynomial.rs:316-365) as a table remainder:
+// C mod S = XOR over the set bits k of C of (X^k mod S), so remainder bit j is the parity of
+// C AND Z_j, where bit k of the row Z_j is bit j of X^k mod S (zt: sdeg rows of acap limbs, built
+// by the host).  The same linear functional as the decrypt table (row j = 0), for every bit of
+// the remainder; identical to the long division's remainder, which is unique.  One wave per
+// polynomial: lanes hold C's limbs, one ballot per remainder bit gives its parity.
+constexpr int kRemLimbsPerLane = 8; // polynomials up to 512 limbs (32768 coefficients)
+
+__global__ void __launch_bounds__(256) poly_rem_kernel(PolyArgs P, const uint64_t *zt, uint32_t sdeg) {
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
     if (e >= P.n) return;
+    const int lane = lane_id();
     const uint64_t *a = P.a + e * P.acap;
     uint64_t *r = P.out + e * P.ocap;
-    const uint32_t deg_a = P.adeg[e];
-    for (uint32_t k = 0; k < P.ocap; ++k) r[k] = k < P.acap ? a[k] : 0ull;
-    const uint32_t sl = sdeg / 64 + 1;
-    int rd = (int)deg_a;
-    while (rd >= (int)sdeg) {
-        if ((r[rd / 64] >> (rd % 64)) & 1ull) {
-            const uint32_t sh = (uint32_t)rd - sdeg, ws = sh / 64, bs = sh % 64;
-            for (uint32_t k = 0; k < sl; ++k) {
-                r[ws + k] ^= S[k] << bs;
-                if (bs && ws + k + 1 < P.ocap) r[ws + k + 1] ^= S[k] >> (64 - bs);
+    const int na = poly_words(a, rfl(P.adeg[e])) ? (int)(rfl(P.adeg[e]) / 64 + 1) : 0;
+    uint64_t c[kRemLimbsPerLane];
+#pragma unroll
+    for (int t = 0; t < kRemLimbsPerLane; ++t) {
+        const int k = lane + kWave * t;
+        c[t] = k < na ? a[k] : 0ull;
+    }
+    // remainder bits, 64 at a time: lane j%64 keeps word j/64's bit j%64
+    // remainder limbs: degree < sdeg, and < 64 acap (a remainder never exceeds its dividend)
+    const int rl = min((int)(sdeg + 63) / 64, (int)P.ocap);
+    int top = -1;
+    for (int w = 0; w < rl; ++w) {
+        uint64_t word = 0ull;
+        for (int jb = 0; jb < 64 && 64 * w + jb < (int)sdeg; ++jb) {
+            const uint64_t *z = zt + (size_t)(64 * w + jb) * P.acap;
+            uint32_t par = 0u;
+#pragma unroll
+            for (int t = 0; t < kRemLimbsPerLane; ++t) {
+                const int k = lane + kWave * t;
+                if (k < na) par ^= (uint32_t)__popcll(c[t] & z[k]);
             }
+            const uint64_t m = __ballot(par & 1u);
+            word |= (uint64_t)(__popcll(m) & 1) << jb;
         }
-        --rd;
+        if (lane == 0) r[w] = word; // word is wave-uniform
+        if (word) top = 64 * w + 63 - __builtin_clzll(word);
     }
-    // exact degree of the remainder (< sdeg)
-    int d = 0;
-    for (int k = (int)min(P.ocap, sl) - 1; k >= 0; --k) {
-        if (r[k]) { d = k * 64 + 63 - __builtin_clzll(r[k]); break; }
-    }
-    P.odeg[e] = (uint32_t)d;
+    for (int k = rl + lane; k < (int)P.ocap; k += kWave) r[k] = 0ull;
+    if (lane == 0) P.odeg[e] = (uint32_t)max(top, 0);
 }
 
 int launch_poly_add(const PolyArgs &P, void *stream) {
@@ -149,10 +165,11 @@ int launch_poly_mul(const PolyArgs &P, void *stream) {
                        (hipStream_t)stream, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_poly_rem(const PolyArgs &P, const uint64_t *S, uint32_t sdeg, void *stream) {
+int launch_poly_rem(const PolyArgs &P, const uint64_t *zt, uint32_t sdeg, void *stream) {
     if (!P.n) return 0;
-    hipLaunchKernelGGL(poly_rem_kernel, dim3((unsigned)((P.n + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, P, S, sdeg);
+    if (P.acap > (uint32_t)(kWave * kRemLimbsPerLane)) return HM_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(poly_rem_kernel, dim3((unsigned)((P.n + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, P, zt, sdeg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -63,7 +63,10 @@ struct MulPlan {
     uint64_t astride = 0; // arena words per value
     std::vector<int64_t> res_bound;
     struct Col {
-        uint32_t pp, npp;          // MulPPTask offset / count (in tasks)
+        uint32_t pp, npp;          // MulPPTask offset / count (in tasks): the VALU partial products
+        uint32_t ppm, ppm_spans, nppm_spans; // MFMA partial products: MulProdTask offset (ppm
+                                             // list), their spans (mspans offset / count)
+        uint32_t ppm_vmax;
         uint32_t items, nitems;    // u32 offset of the item slot ids
         uint32_t prefix;           // u32 offset of the prefix slot ids (nitems - 1)
         uint32_t res;              // result degree slot
@@ -81,6 +84,7 @@ struct MulPlan {
     std::vector<MulProdTask> prod;
     std::vector<MulTile> tiles;
     std::vector<MulTile> mspans; // MFMA spans {task, first output word} of the schoolbook products
+    std::vector<MulProdTask> ppm; // partial products a_j * b_k run on the matrix cores
     std::vector<KaSum> ka_sums;
     std::vector<MulVTask> ka_vtasks;
     std::vector<MulVTile> ka_vtiles;
@@ -88,7 +92,7 @@ struct MulPlan {
     uint8_t *d_tab = nullptr;
     size_t tab_bytes = 0;
     size_t off_slots = 0, off_pp = 0, off_lists = 0, off_prod = 0, off_tiles = 0, off_res = 0;
-    size_t off_mspans = 0;
+    size_t off_mspans = 0, off_ppm = 0;
     size_t off_ka_sums = 0, off_ka_vtasks = 0, off_ka_vtiles = 0, off_ka_combs = 0;
     uint64_t work = 0; // word-pair products (statistics)
 };
@@ -208,14 +212,31 @@ bool build_plan(MulPlan &P) {
         reg[creg].used = 0;
         std::vector<Item> items;
         col.pp = (uint32_t)P.pp.size();
+        col.ppm = (uint32_t)P.ppm.size(), col.ppm_vmax = 0;
+        std::vector<MulTile> ppm_spans;
         for (uint32_t j = 0; j <= i; ++j) {
             const int64_t bnd = (int64_t)P.ab[j] + P.bb[i - j];
             if (bnd > kBoundLimit) return false;
             const uint32_t s = new_slot(PP, bnd);
-            P.pp.push_back({j, K + (i - j), s, pp_flip(P.is_signed, P.L, i, j) ? 1u : 0u});
+            const bool flip = pp_flip(P.is_signed, P.L, i, j);
+            const uint32_t sa = j, sb = K + (i - j);
+            const uint32_t wa = P.slots[sa].words, wb = P.slots[sb].words;
+            // on the matrix cores unless a signed corner (+1) or a narrow operand
+            if (P.mfma && !flip && std::min(wa, wb) >= kMfMinWords) {
+                const uint32_t t = (uint32_t)P.ppm.size() - col.ppm;
+                P.ppm.push_back(wa <= wb ? MulProdTask{sa, sb, s} : MulProdTask{sb, sa, s});
+                for (uint32_t base = 0; base < P.slots[s].words; base += 32 * kMfSpan)
+                    ppm_spans.push_back({t, base});
+                col.ppm_vmax = std::max(col.ppm_vmax, std::max(wa, wb));
+            } else {
+                P.pp.push_back({sa, sb, s, flip ? 1u : 0u});
+            }
             items.push_back({s, bnd});
         }
         col.npp = (uint32_t)P.pp.size() - col.pp;
+        col.ppm_spans = (uint32_t)P.mspans.size();
+        P.mspans.insert(P.mspans.end(), ppm_spans.begin(), ppm_spans.end());
+        col.nppm_spans = (uint32_t)ppm_spans.size();
         items.insert(items.end(), prev.begin(), prev.end());
         const bool push = i + 1 < K;
         std::vector<Item> cur;
@@ -369,6 +390,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
     P.off_mspans = o, o = align(o + P.mspans.size() * sizeof(MulTile));
+    P.off_ppm = o, o = align(o + P.ppm.size() * sizeof(MulProdTask));
     P.off_ka_sums = o, o = align(o + P.ka_sums.size() * sizeof(KaSum));
     P.off_ka_vtasks = o, o = align(o + P.ka_vtasks.size() * sizeof(MulVTask));
     P.off_ka_vtiles = o, o = align(o + P.ka_vtiles.size() * sizeof(MulVTile));
@@ -384,6 +406,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
     put(P.off_mspans, P.mspans.data(), P.mspans.size() * sizeof(MulTile));
+    put(P.off_ppm, P.ppm.data(), P.ppm.size() * sizeof(MulProdTask));
     put(P.off_ka_sums, P.ka_sums.data(), P.ka_sums.size() * sizeof(KaSum));
     put(P.off_ka_vtasks, P.ka_vtasks.data(), P.ka_vtasks.size() * sizeof(MulVTask));
     put(P.off_ka_vtiles, P.ka_vtiles.data(), P.ka_vtiles.size() * sizeof(MulVTile));
@@ -563,6 +586,14 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             MulPPArgs pp{};
             pp.B = B, pp.tasks = (const MulPPTask *)(T + P->off_pp) + col.pp, pp.ntasks = col.npp;
             if (launch_mul_pp(pp, c->stream)) return hip_fail(c, hipGetLastError());
+            if (col.nppm_spans) {
+                MulMfmaArgs mf{};
+                mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_ppm) + col.ppm;
+                mf.spans = (const MulTile *)(T + P->off_mspans) + col.ppm_spans;
+                mf.nitems = col.nppm_spans, mf.span = kMfSpan;
+                mf.vmax = col.ppm_vmax, mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span);
+                if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
+            }
             MulScanArgs sc{};
             sc.B = B;
             sc.items = (const uint32_t *)(T + P->off_lists) + col.items;

@@ -186,7 +186,11 @@ mul_mfma_kernel(MulMfmaArgs P) {
         for (; c0 + kMfG + (fold ? 1 : 0) < nc + (fold ? 0 : 1); c0 += kMfG)
             mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
         if (fold) mf_group<kMfG + 1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += kMfG + 1;
-        for (; c0 + 4 <= nc; c0 += 4) mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        // then groups of 4, the last one taking a fifth chunk when one would be left over
+        while (nc - c0 >= 4) {
+            if (nc - c0 == 5) mf_group<5>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += 5;
+            else mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += 4;
+        }
         for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
     }
     wsync();
