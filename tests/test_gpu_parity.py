@@ -73,7 +73,8 @@ def test_poly_mul_add(H, oracle, ca, cb):
         assert np.array_equal(sl[i, :w], ref[:w]) and not sl[i, w:].any()
 
 
-@pytest.mark.parametrize("cap,sdeg", [(1, 1), (3, 128), (20, 128), (9, 63), (9, 64), (50, 700)])
+@pytest.mark.parametrize("cap,sdeg", [(1, 1), (3, 128), (20, 128), (9, 63), (9, 64), (50, 700),
+                                      (369, 128), (512, 256), (4, 300)])
 def test_poly_rem(H, oracle, cap, sdeg):
     rng = np.random.default_rng(cap + sdeg)
     A = _rand_polys(rng, 64, cap)
