@@ -579,6 +579,7 @@ def run_add(args, world, rank, device):
     """configs[1]: u32 homomorphic add, batch 4096 per GPU (weak scaling)."""
     ctx = make_context(world, rank, device)
     ctx.set_add_pipeline(bool(args.add_pipeline))
+    ctx.set_add_options(args.add_chain)
     n = args.batch or 4096
     a, b = shard_inputs(rank, n)
     ca, cb = ctx.encrypt(a), ctx.encrypt(b)  # masks from the (seeded) engine CSPRNG
@@ -648,6 +649,7 @@ def run_add(args, world, rank, device):
         "data": "synthetic: seeded u32 plaintexts, seeded keys, subset masks from the seeded engine CSPRNG",
         "config": {"workload": "u32 homomorphic add (configs[1])", "global_batch": n * world,
                    "add_pipeline": bool(args.add_pipeline),
+                   "add_chain": args.add_chain,
                    "batch_per_gpu": n, "d": PARAMS[0], "dp": PARAMS[1], "delta": PARAMS[2],
                    "tau": PARAMS[3], "parallelism": f"batch-sharded x{world}"},
         "verified": {"correct_sums": correct, "of": n * world},
@@ -807,6 +809,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--add-chain", choices=["auto", "mfma", "valu"], default="auto",
+                    help="hm_ctx_set_add_options (auto = the MFMA chain where it applies)")
     ap.add_argument("--add-pipeline", type=int, default=0,
                     help="1: big adds run as two pipelined halves; 0: one pass (engine default)")
     ap.add_argument("--graph", type=int, default=1,

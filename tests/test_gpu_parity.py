@@ -159,6 +159,7 @@ def _pair(H, ctx, params, dtype, n, seed, lo=None, hi=None):
 @pytest.mark.parametrize("chain", ["auto", "mfma", "valu"])
 @pytest.mark.parametrize("params,dtype,n", [((64, 64, 1, 64), np.uint8, 128),
                                             ((64, 64, 1, 64), np.uint32, 32),
+                                            ((128, 128, 1, 128), np.uint32, 7),
                                             ((64, 16, 1, 16), np.uint8, 64),
                                             ((128, 128, 1, 128), np.uint32, 24),
                                             ((128, 128, 4, 128), np.uint16, 32),
