@@ -237,7 +237,10 @@ int launch_encrypt(const EncArgs &E, void *stream) {
 // ---------------------------------------------------------------------------------------------
 // Decryption: bit = parity(C & z) with z_k = (X^k mod S)(0).  Wide ciphertexts (circuit outputs):
 // one wavefront per value; lanes stride over the value's limbs (coalesced), accumulate per-bit
-// parities, XOR-reduce.
+// parities, XOR-reduce.  Limbs go kDecUnroll per lane at a time: their bits and z indices first
+// (ALU only), then all their limb and z loads together, so each lane has 2 kDecUnroll loads in
+// flight instead of one dependent pair.
+constexpr uint32_t kDecUnroll = 8;
 __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
     const int wave = (int)rfl(threadIdx.x >> 6);
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -249,20 +252,33 @@ __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
     // bit i of the value owns limbs [lo, hi); each lane walks its limbs in increasing order
     uint32_t i = 0, lo = 0, hi = cap_of(D.ib.b[0]);
     bool bad = false;
-    for (uint32_t g = lane; g < total; g += kWave) {
-        while (g >= hi) {
-            ++i;
-            lo = hi;
-            hi += cap_of(D.ib.b[i]);
+    for (uint32_t g0 = lane; g0 < total; g0 += kDecUnroll * kWave) {
+        uint32_t bi[kDecUnroll], zi[kDecUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kDecUnroll; ++u) {
+            const uint32_t g = g0 + u * kWave;
+            if (g < total)
+                while (g >= hi) {
+                    ++i;
+                    lo = hi;
+                    hi += cap_of(D.ib.b[i]);
+                }
+            bi[u] = i, zi[u] = g - lo;
         }
-        const uint64_t v = src[g];
-        const uint32_t zi = g - lo;
-        uint64_t z = 0;
-        if (zi < D.zlimbs) z = D.z[zi];
-        else if (v) bad = true;
-        const uint64_t p = (uint64_t)(__builtin_popcountll(v & z) & 1);
-        if (i < 64) m0 ^= p << i;
-        else m1 ^= p << (i - 64);
+        uint64_t v[kDecUnroll], z[kDecUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kDecUnroll; ++u) {
+            const uint32_t g = g0 + u * kWave;
+            v[u] = g < total ? src[g] : 0ull;
+            z[u] = zi[u] < D.zlimbs ? D.z[zi[u]] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kDecUnroll; ++u) {
+            if (zi[u] >= D.zlimbs && v[u]) bad = true;
+            const uint64_t p = (uint64_t)(__builtin_popcountll(v[u] & z[u]) & 1);
+            if (bi[u] < 64) m0 ^= p << bi[u];
+            else m1 ^= p << (bi[u] - 64);
+        }
     }
     if (__any(bad) && lane == 0) flag(D.status, HM_ERR_UNSUPPORTED);
     const uint32_t r0 = wave_xor_u32((uint32_t)m0), r1 = wave_xor_u32((uint32_t)(m0 >> 32));
