@@ -15,10 +15,10 @@
 // and across blocks OUT, the span's output words, XOR-accumulated.  Chunks (floor(ub/2) + 1 of
 // K = 64) are taken in groups of G (16, then 4, then 1 for the tail): the group's A fragments are
 // built once, then every tile of the span that the group reaches is swept, two tiles at a time
-// (independent accumulator chains), one B read per chunk and tile.  The two accumulator sets
-// start at 2^23 once per block and keep counting; the parity change over one (tile, group) is its
-// part of the product mod 2, and parts of different groups and blocks meet in OUT by XOR (the
-// parity of a sum is the XOR of the parities of its parts).
+// (independent accumulator chains), one B read per chunk and tile.  Each (tile, group) starts its
+// accumulators at 2^23, so its parities are its part of the product mod 2; parts of different
+// groups and blocks meet in OUT by XOR (the parity of a sum is the XOR of the parities of its
+// parts).
 #include <hip/hip_runtime.h>
 
 #include "mfma_gf2.h"
@@ -42,21 +42,22 @@ __host__ __device__ constexpr uint32_t mf_wave_words(uint32_t vmax, uint32_t spa
 
 __device__ __forceinline__ int floor_div32(int x) { return x >= 0 ? x / 32 : -((31 - x) / 32); }
 
-// Tiles T0 .. T0 + NT - 1 (NT = 1, 2) against G chunks from c0: accumulator set t per tile, one
-// B read per chunk and tile (window word 32T + col - D + h + 2c of VI, whose first word is vlo),
-// the parities XORed into OUT (span-relative tile T - Ts).  The accumulator sets are not reset
-// per (group, tile): they keep counting from 2^23 over the whole U block (below 2^24: at most
-// 129 chunks x 16 tiles x 64 per accumulator), and a tile's parities are bit 0 now XOR bit 0
-// before it (gp), which saves the 16 moves of a reset per tile.
+// Tiles T0 .. T0 + NT - 1 (NT = 1, 2) against G chunks from c0: one accumulator set per tile,
+// one B read per chunk and tile (window word 32T + col - D + h + 2c of VI, whose first word is
+// vlo), the parities XORed into OUT (span-relative tile T - Ts).
 template <int G, int NT>
 __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI, int vlo, int T0,
-                                         int Ts, int c0, int D, uint32_t *OUT, v16f (&acc)[2],
-                                         uint32_t (&gp)[2]) {
+                                         int Ts, int c0, int D, uint32_t *OUT) {
     const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
     const uint4 *bt[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
         bt[t] = (const uint4 *)VI + (32 * (T0 + t) + col - D + h + 2 * c0 - vlo);
+    v16f acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[t][j] = 8388608.0f;
     constexpr int P = G < kMfPf ? G : kMfPf;
     uint4 bq[NT][G];
 #pragma unroll
@@ -78,9 +79,7 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const uint32_t now = acc_parities(acc[t]);
-        const uint32_t word = join_halves((now ^ gp[t]) << (4 * h));
-        gp[t] = now;
+        const uint32_t word = join_halves(acc_parities(acc[t]) << (4 * h));
         if (h == 0) atomicXor(&OUT[32 * (T0 + t - Ts) + col], word); // this wave's slice only
     }
 }
@@ -88,8 +87,7 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
 // One group of G chunks from c0 over the tiles tlo .. thi of the span
 template <int G>
 __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
-                                         int nv, int Ts, int Te, int c0, uint32_t *OUT,
-                                         v16f (&acc)[2], uint32_t (&gp)[2]) {
+                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
     const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
     const int jb = 32 * (R - D + h) - 1 - col;
     const uint32_t *rw0 = RS + (jb >> 3) + 8 * c0;
@@ -101,8 +99,8 @@ __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI,
     const int tlo = max(Ts, floor_div32(D - 2 * c0 - 2 * G + 1));
     const int thi = min(Te - 1, floor_div32(nv - 1 + D - 2 * c0));
     int T = tlo;
-    for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT, acc, gp);
-    if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT, acc, gp);
+    for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT);
+    if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
 }
 
 template <bool LEAF>
@@ -178,12 +176,6 @@ mul_mfma_kernel(MulMfmaArgs P) {
             ((uint4 *)VI)[i] = q;
         }
         wsync();
-        v16f acc[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) acc[t][j] = 8388608.0f;
-        uint32_t gp[2] = {0u, 0u};
         const int tlo = max(Ts, 0);
         uint32_t *OUTs = OUT + 32 * (tlo - Ts);
         // groups of 16 chunks; a block of 2 mod 32 words (nc = 1 mod 16, e.g. the 129 chunks of a
@@ -192,14 +184,14 @@ mul_mfma_kernel(MulMfmaArgs P) {
         const bool fold = nc % kMfG == 1 && nc > kMfG;
         int c0 = 0;
         for (; c0 + kMfG + (fold ? 1 : 0) < nc + (fold ? 0 : 1); c0 += kMfG)
-            mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, acc, gp);
-        if (fold) mf_group<kMfG + 1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, acc, gp), c0 += kMfG + 1;
+            mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        if (fold) mf_group<kMfG + 1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += kMfG + 1;
         // then groups of 4, the last one taking a fifth chunk when one would be left over
         while (nc - c0 >= 4) {
-            if (nc - c0 == 5) mf_group<5>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, acc, gp), c0 += 5;
-            else mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, acc, gp), c0 += 4;
+            if (nc - c0 == 5) mf_group<5>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += 5;
+            else mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += 4;
         }
-        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, acc, gp);
+        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
     }
     wsync();
     for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
