@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-B="python3 bench.py --steps 20 --warmup 3 --no-cpu --no-secondary"
+B="python3 bench.py --no-cpu --no-secondary"
 run() { local name=$1; shift; timeout -k 10 400 "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "[$name] rc=$rc"; tail -n 2 $OUT/$name.log; [ $rc -eq 0 ] || exit $rc; }
 run trace rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py
 run fetch rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B

@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
@@ -16,7 +17,8 @@ batch = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 per = {}
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
+        # kernel name without return type and template arguments ("hm::add_chain_mfma_kernel")
+        k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0]).replace("void ", "")
         if "add_" not in k or r["Counter_Name"] not in (
                 "FETCH_SIZE", "WRITE_SIZE", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES",
                 "SQ_ACTIVE_INST_VALU"):
