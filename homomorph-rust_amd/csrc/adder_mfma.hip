@@ -186,7 +186,7 @@ add_chain_mfma_kernel(AddArgs A) {
     stage_rec(0);
 
 #ifdef HM_MFMA_PROFILE
-    unsigned long long prof[3] = {0, 0, 0};
+    unsigned long long prof[4] = {0, 0, 0, 0};
 #endif
     for (uint32_t k = lane; k < Cfg::kHalo + A.mf_cw; k += kWave) Ls[k] = 0u;
     for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u; // P below bit 0
@@ -196,10 +196,12 @@ add_chain_mfma_kernel(AddArgs A) {
     int tw = -1;   // > 0: the previous bit's tiles stored sum words [cntX, min(tw, cap words))
     uint32_t offo = 0;
     for (uint32_t i = 0; i < L; ++i) {
+        HM_PT(tw0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
         const uint32_t *rec = &stage[wave][i & 1][0];
         // s_i = x_i ^ carry_i (common.rs:43-47)
         HM_PT(t0);
+        HM_PACC(3, tw0, t0);
         if (tw < 0) {
             store_sum_x(rec, (int)A.cntX, C, nc, po + offo, A.ob.b[i], dout + i, A.status);
         } else {
@@ -362,7 +364,7 @@ add_chain_mfma_kernel(AddArgs A) {
     }
 #ifdef HM_MFMA_PROFILE
     if (lane == 0)
-        for (int k = 0; k < 3; ++k) g_mfma_prof[e * 4 + k] = prof[k];
+        for (int k = 0; k < 4; ++k) g_mfma_prof[e * 4 + k] = prof[k];
 #endif
 }
 

@@ -121,44 +121,73 @@ int launch_mul_pp(const MulPPArgs &P, void *stream) {
 // one wave per (value, 256-word chunk): acc ^= x_t chunk, store p_{t+1} chunk, track degrees.
 // Slots are zero above their degree and capacities are multiples of 4 words, so every item and
 // prefix is read / written as whole uint4s up to its capacity.
+//   - The column's slot records (item t, and the slot that receives p_{t+1} or the output bit)
+//     are copied into LDS once per block: read per item through items[] -> slots[], they were
+//     two dependent scalar loads each, twice per item, and the kernel waited ~90 % of its cycles.
+//   - Items live in the pp / carry regions and prefixes in their own region (mul_host.cpp
+//     build_plan), so no store aliases a later item: kScanBatch item loads are issued together,
+//     ahead of the XORs and stores.
+constexpr uint32_t kScanBatch = 8;
+
 __global__ void __launch_bounds__(256) mul_scan_kernel(MulScanArgs S) {
+    extern __shared__ uint32_t lds[]; // [item off][item words][dest off][dest words][dest slot] x nitems
+    uint32_t *ioff = lds, *iwords = lds + S.nitems, *doff = lds + 2 * S.nitems, *dwords = lds + 3 * S.nitems;
+    uint32_t *dslots = lds + 4 * S.nitems;
+    for (uint32_t t = threadIdx.x; t < S.nitems; t += blockDim.x) {
+        const MulSlot si = S.B.slots[S.items[t]];
+        ioff[t] = si.off, iwords[t] = si.words;
+        if (t + 1 < S.nitems) {
+            const MulSlot sp = S.B.slots[S.prefix[t]];
+            doff[t] = sp.off, dwords[t] = sp.words, dslots[t] = S.prefix[t];
+        } else {
+            doff[t] = 0u, dwords[t] = 0u, dslots[t] = S.res; // the output bit
+        }
+    }
+    __syncthreads();
     const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
     const uint64_t e = g / S.chunks;
     const uint32_t c0 = (uint32_t)(g % S.chunks) * 256u;
     if (e >= S.B.nv) return;
     const int lane = lane_id();
     const uint32_t w = c0 + 4u * (uint32_t)lane;
+    uint32_t *const arena = S.B.arena + e * S.B.astride;
     uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t t = 0; t < S.nitems; ++t) {
-        const uint32_t it = S.items[t];
-        const MulSlot si = S.B.slots[it];
-        if (w < si.words) {
-            const uint4 v = *(const uint4 *)(S.B.arena + e * S.B.astride + si.off + w);
-            acc.x ^= v.x, acc.y ^= v.y, acc.z ^= v.z, acc.w ^= v.w;
+    for (uint32_t t0 = 0; t0 < S.nitems; t0 += kScanBatch) {
+        const uint32_t nb = min(kScanBatch, S.nitems - t0);
+        uint4 v[kScanBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kScanBatch; ++k) {
+            v[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (k < nb && w < iwords[t0 + k]) v[k] = *(const uint4 *)(arena + ioff[t0 + k] + w);
         }
-        int tw = -1;
-        uint32_t tv = 0;
-        if (acc.x) tw = (int)w, tv = acc.x;
-        if (acc.y) tw = (int)w + 1, tv = acc.y;
-        if (acc.z) tw = (int)w + 2, tv = acc.z;
-        if (acc.w) tw = (int)w + 3, tv = acc.w;
-        const uint32_t dslot = t + 1 < S.nitems ? S.prefix[t] : S.res;
-        if (t + 1 < S.nitems) {
-            const MulSlot sp = S.B.slots[dslot];
-            if (w < sp.words) *(uint4 *)(S.B.arena + e * S.B.astride + sp.off + w) = acc;
-        } else {
-            // the output bit: u32 words into the u64 limbs (little-endian), zeros up to capacity
-            uint32_t *o = (uint32_t *)(S.out.limbs + (S.B.e0 + e) * S.out.stride + S.out_off);
-            const uint32_t ow = 2 * S.out_cap;
-            if (w < ow) *(uint2 *)(o + w) = make_uint2(acc.x, acc.y);
-            if (w + 2 < ow) *(uint2 *)(o + w + 2) = make_uint2(acc.z, acc.w);
-        }
-        // degree + 1 of this prefix: the chunk's top bit, max over chunks
-        const uint64_t m = __ballot(tw >= 0);
-        if (m) {
-            const int hl = 63 - __builtin_clzll(m);
-            if (lane == hl) atomicMax(&S.B.deg1[(uint64_t)dslot * S.B.nv + e],
-                                      (uint32_t)(tw * 32 + 32 - __builtin_clz(tv)));
+#pragma unroll
+        for (uint32_t k = 0; k < kScanBatch; ++k) {
+            if (k >= nb) break;
+            const uint32_t t = t0 + k;
+            acc.x ^= v[k].x, acc.y ^= v[k].y, acc.z ^= v[k].z, acc.w ^= v[k].w;
+            int tw = -1;
+            uint32_t tv = 0;
+            if (acc.x) tw = (int)w, tv = acc.x;
+            if (acc.y) tw = (int)w + 1, tv = acc.y;
+            if (acc.z) tw = (int)w + 2, tv = acc.z;
+            if (acc.w) tw = (int)w + 3, tv = acc.w;
+            if (t + 1 < S.nitems) {
+                if (w < dwords[t]) *(uint4 *)(arena + doff[t] + w) = acc;
+            } else {
+                // the output bit: u32 words into the u64 limbs (little-endian), zeros up to capacity
+                uint32_t *o = (uint32_t *)(S.out.limbs + (S.B.e0 + e) * S.out.stride + S.out_off);
+                const uint32_t ow = 2 * S.out_cap;
+                if (w < ow) *(uint2 *)(o + w) = make_uint2(acc.x, acc.y);
+                if (w + 2 < ow) *(uint2 *)(o + w + 2) = make_uint2(acc.z, acc.w);
+            }
+            // degree + 1 of this prefix: the chunk's top bit, max over chunks
+            const uint64_t m = __ballot(tw >= 0);
+            if (m) {
+                const uint32_t dslot = dslots[t];
+                const int hl = 63 - __builtin_clzll(m);
+                if (lane == hl) atomicMax(&S.B.deg1[(uint64_t)dslot * S.B.nv + e],
+                                          (uint32_t)(tw * 32 + 32 - __builtin_clz(tv)));
+            }
         }
     }
 }
@@ -166,8 +195,9 @@ __global__ void __launch_bounds__(256) mul_scan_kernel(MulScanArgs S) {
 int launch_mul_scan(const MulScanArgs &S, void *stream) {
     const uint64_t waves = S.B.nv * S.chunks;
     if (!waves || !S.nitems) return 0;
-    hipLaunchKernelGGL(mul_scan_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, S);
+    if ((size_t)S.nitems * 20 > 64 * 1024) return -1; // slot records staged in LDS
+    hipLaunchKernelGGL(mul_scan_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256),
+                       (size_t)S.nitems * 20, (hipStream_t)stream, S);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
