@@ -188,6 +188,7 @@ struct MulMfmaArgs {
     uint32_t nspans;      // leaves: spans per task
     uint32_t span;        // output tiles per span
     uint32_t vmax, wave_words;
+    uint32_t umax;        // largest U (words; blocks of at most kMfUB): sizes the U image
 };
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
 struct KaComb {
@@ -255,7 +256,7 @@ int launch_mul_final(const MulFinalArgs &a, void *stream);
 int launch_ka_sum(const KaSumArgs &a, void *stream);
 int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
-uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span);
+uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);
 int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches

@@ -66,14 +66,14 @@ struct MulPlan {
         uint32_t pp, npp;          // MulPPTask offset / count (in tasks): the VALU partial products
         uint32_t ppm, ppm_spans, nppm_spans; // MFMA partial products: MulProdTask offset (ppm
                                              // list), their spans (mspans offset / count)
-        uint32_t ppm_vmax;
+        uint32_t ppm_vmax, ppm_umax;
         uint32_t items, nitems;    // u32 offset of the item slot ids
         uint32_t prefix;           // u32 offset of the prefix slot ids (nitems - 1)
         uint32_t res;              // result degree slot
         uint32_t maxwords;         // widest prefix / result
         uint32_t prod;             // MulProdTask offset (in tasks)
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
-        uint32_t mspans, nmspans, mvmax;  // MFMA products: MulTile spans (offset / count), max V
+        uint32_t mspans, nmspans, mvmax, mumax;  // MFMA products: MulTile spans (offset / count), max V
         std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
@@ -212,7 +212,7 @@ bool build_plan(MulPlan &P) {
         reg[creg].used = 0;
         std::vector<Item> items;
         col.pp = (uint32_t)P.pp.size();
-        col.ppm = (uint32_t)P.ppm.size(), col.ppm_vmax = 0;
+        col.ppm = (uint32_t)P.ppm.size(), col.ppm_vmax = 0, col.ppm_umax = 0;
         std::vector<MulTile> ppm_spans;
         for (uint32_t j = 0; j <= i; ++j) {
             const int64_t bnd = (int64_t)P.ab[j] + P.bb[i - j];
@@ -228,6 +228,7 @@ bool build_plan(MulPlan &P) {
                 for (uint32_t base = 0; base < P.slots[s].words; base += 32 * kMfSpan)
                     ppm_spans.push_back({t, base});
                 col.ppm_vmax = std::max(col.ppm_vmax, std::max(wa, wb));
+                col.ppm_umax = std::max(col.ppm_umax, std::min(wa, wb));
             } else {
                 P.pp.push_back({sa, sb, s, flip ? 1u : 0u});
             }
@@ -329,7 +330,7 @@ bool build_plan(MulPlan &P) {
         // tiles of this column's schoolbook products: MFMA spans where the uniform operand has
         // at least kMfMinWords words (mfma plans), the rest grouped by per-lane VALU tile width
         std::vector<MulTile> byw[kNW];
-        col.mspans = (uint32_t)P.mspans.size(), col.mvmax = 0;
+        col.mspans = (uint32_t)P.mspans.size(), col.mvmax = 0, col.mumax = 0;
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
             if (is_ka[k - col.prod]) continue;
             if (P.mfma && P.slots[P.prod[k].u].words >= kMfMinWords) {
@@ -337,6 +338,7 @@ bool build_plan(MulPlan &P) {
                 for (uint32_t base = 0; base < nout; base += 32 * kMfSpan)
                     P.mspans.push_back({k - col.prod, base});
                 col.mvmax = std::max(col.mvmax, P.slots[P.prod[k].v].words);
+                col.mumax = std::max(col.mumax, P.slots[P.prod[k].u].words);
                 continue;
             }
             const uint32_t nout = P.slots[P.prod[k].out].words;
@@ -516,7 +518,8 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         a.span = std::max(1u, (pg.leaf_omax + 31) / 32); // one span: the whole leaf output
         a.nspans = 1;
         a.nitems = pg.nvtask;
-        a.vmax = pg.leaf_vmax, a.wave_words = mul_mfma_wave_words(a.vmax, a.span);
+        a.vmax = pg.leaf_vmax, a.umax = pg.leaf_umax;
+        a.wave_words = mul_mfma_wave_words(a.vmax, a.span, a.umax);
         if (launch_mul_mfma(a, true, c->stream)) return hip_fail(c, hipGetLastError());
     } else {
         for (uint32_t q = 0; q < kNW; ++q) {
@@ -591,7 +594,8 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_ppm) + col.ppm;
                 mf.spans = (const MulTile *)(T + P->off_mspans) + col.ppm_spans;
                 mf.nitems = col.nppm_spans, mf.span = kMfSpan;
-                mf.vmax = col.ppm_vmax, mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span);
+                mf.vmax = col.ppm_vmax, mf.umax = col.ppm_umax;
+                mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span, mf.umax);
                 if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
             }
             MulScanArgs sc{};
@@ -608,7 +612,8 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_prod) + col.prod;
                 mf.spans = (const MulTile *)(T + P->off_mspans) + col.mspans;
                 mf.nitems = col.nmspans, mf.span = kMfSpan;
-                mf.vmax = col.mvmax, mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span);
+                mf.vmax = col.mvmax, mf.umax = col.mumax;
+                mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span, mf.umax);
                 if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
             }
             for (uint32_t q = 0; q < kNW; ++q) {

@@ -29,15 +29,18 @@ constexpr int kMfG = 16;      // chunks per full A group (64 VGPRs of A fragment
 constexpr int kMfPf = 3;      // B reads issued ahead of their MFMA
 constexpr int kVPad = 2 * kMfG + 32; // V words read beyond V's ends (zero)
 
-__host__ __device__ constexpr uint32_t mf_rs_words() { return 4 * (kMfUB + 2) + 16; }
-// V words one (block, span) reaches: 32 span + 32 + 2 NC (NC <= kMfUB/2 + 1), or all of V plus
-// its zero pads when that is fewer
-__host__ __device__ constexpr uint32_t mf_vi_words(uint32_t vmax, uint32_t span) {
-    const uint32_t a = 32 * span + 32 + 2 * (kMfUB / 2 + 1), b = vmax + 2 * kVPad;
+// U blocks of at most ub = min(umax, kMfUB) words: the launch's LDS slices are sized for them
+// (a launch of narrow schoolbook products reserves no 256-word U image, so more waves fit a CU)
+__host__ __device__ constexpr uint32_t mf_ub(uint32_t umax) { return umax < kMfUB ? umax : kMfUB; }
+__host__ __device__ constexpr uint32_t mf_rs_words(uint32_t umax) { return 4 * (mf_ub(umax) + 2) + 16; }
+// V words one (block, span) reaches: 32 span + 32 + 2 NC (NC <= ub/2 + 1), or all of V plus its
+// zero pads when that is fewer
+__host__ __device__ constexpr uint32_t mf_vi_words(uint32_t vmax, uint32_t span, uint32_t umax) {
+    const uint32_t a = 32 * span + 32 + 2 * (mf_ub(umax) / 2 + 1), b = vmax + 2 * kVPad;
     return 4 * ((a < b ? a : b) + 8);
 }
-__host__ __device__ constexpr uint32_t mf_wave_words(uint32_t vmax, uint32_t span) {
-    return mf_rs_words() + mf_vi_words(vmax, span) + 32 * span;
+__host__ __device__ constexpr uint32_t mf_wave_words(uint32_t vmax, uint32_t span, uint32_t umax) {
+    return mf_rs_words(umax) + mf_vi_words(vmax, span, umax) + 32 * span;
 }
 
 __device__ __forceinline__ int floor_div32(int x) { return x >= 0 ? x / 32 : -((31 - x) / 32); }
@@ -145,8 +148,9 @@ mul_mfma_kernel(MulMfmaArgs P) {
         return;
     }
     uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
-    uint32_t *VI = RS + mf_rs_words();
-    uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span);
+    const uint32_t rs_words = mf_rs_words(P.umax);
+    uint32_t *VI = RS + rs_words;
+    uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
     for (int w = lane; w < 32 * span; w += kWave) OUT[w] = 0u;
     const int T0 = base >> 5;
     for (int b0 = 0; b0 < nu; b0 += kMfUB) {
@@ -166,7 +170,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
             x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
             ((uint4 *)RS)[R - 1 - q] = x;
         }
-        for (int k = 4 * R + lane; k < (int)mf_rs_words(); k += kWave) RS[k] = 0u;
+        for (int k = 4 * R + lane; k < (int)rs_words; k += kWave) RS[k] = 0u;
         for (int i = lane; i < vhi - vlo; i += kWave) {
             const int w = vlo + i;
             const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
@@ -207,6 +211,8 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span) { return mf_wave_words(vmax, span); }
+uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax) {
+    return mf_wave_words(vmax, span, umax);
+}
 
 } // namespace hm
