@@ -28,7 +28,10 @@ constexpr int64_t kBoundLimit = (int64_t)1 << 30;
 constexpr uint32_t kNW = sizeof(kMulTileW) / sizeof(kMulTileW[0]);
 // schoolbook products whose uniform operand has at least this many words run on the matrix cores
 // (mfma plans); narrower ones keep the VALU tiles
-constexpr uint32_t kMfMinWords = 4;
+#ifndef HM_MF_MIN_WORDS
+#define HM_MF_MIN_WORDS 4
+#endif
+constexpr uint32_t kMfMinWords = HM_MF_MIN_WORDS;
 
 inline uint32_t slot_words(int64_t bound) { return ((uint32_t)(bound / 32) + 1 + 3) & ~3u; }
 
