@@ -151,7 +151,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
     const uint32_t rs_words = mf_rs_words(P.umax);
     uint32_t *VI = RS + rs_words;
     uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
-    for (int w = lane; w < 32 * span; w += kWave) OUT[w] = 0u;
+    for (int w = lane; w < wend - base; w += kWave) OUT[w] = 0u; // the span's live words
     const int T0 = base >> 5;
     for (int b0 = 0; b0 < nu; b0 += kMfUB) {
         // U_b = words [b0, b0 + ub) of U: its product with V lands kb = b0/32 tiles up
@@ -182,20 +182,21 @@ mul_mfma_kernel(MulMfmaArgs P) {
         wsync();
         const int tlo = max(Ts, 0);
         uint32_t *OUTs = OUT + 32 * (tlo - Ts);
-        // groups of 16 chunks; a block of 2 mod 32 words (nc = 1 mod 16, e.g. the 129 chunks of a
-        // 256-word leaf) folds its odd chunk into the last group instead of a 1-chunk pass (whose
-        // parity gathers would cost as much as its MFMAs)
-        const bool fold = nc % kMfG == 1 && nc > kMfG;
+        // groups of 16 chunks while more than 17 are left, then the rest as ONE group of 1..17
+        // chunks: every group costs a parity gather per tile it reaches, so a narrow U (the
+        // 17-word partial products at d + d' = 512: 9 chunks) takes one gather per tile instead of
+        // one per 4-chunk group, and a 256-word leaf's 129 chunks end in a 17-chunk group
         int c0 = 0;
-        for (; c0 + kMfG + (fold ? 1 : 0) < nc + (fold ? 0 : 1); c0 += kMfG)
-            mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
-        if (fold) mf_group<kMfG + 1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += kMfG + 1;
-        // then groups of 4, the last one taking a fifth chunk when one would be left over
-        while (nc - c0 >= 4) {
-            if (nc - c0 == 5) mf_group<5>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += 5;
-            else mf_group<4>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs), c0 += 4;
+        for (; nc - c0 > kMfG + 1; c0 += kMfG) mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        switch (nc - c0) {
+#define HM_MF_TAIL(G) \
+    case G: mf_group<G>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs); break;
+            HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
+            HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)
+            HM_MF_TAIL(13) HM_MF_TAIL(14) HM_MF_TAIL(15) HM_MF_TAIL(16) HM_MF_TAIL(17)
+#undef HM_MF_TAIL
+        default: break;
         }
-        for (; c0 < nc; ++c0) mf_group<1>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
     }
     wsync();
     for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
