@@ -72,6 +72,7 @@ __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[NC], const uint4 *rb, 
     // pf holds this tile's first kPrefetch B fragments (read during the tile before); the last
     // kPrefetch reads of this tile fetch the next tile's (window base rbn; its ring fill is side
     // stage 2, issued above them), so the next tile's first MFMA does not wait for the LDS
+    static_assert(NC - kPrefetch > 7, "next tile's B reads must follow its ring fill (stage 2, after MFMA 7)");
     uint4 bq[NC];
 #pragma unroll
     for (int c = 0; c < kPrefetch; ++c) bq[c] = pf[c];

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/ab_mixed; mkdir -p $OUT
 for v in "$@"; do
-  HOMOMORPH_GPU_LIB=$PWD/homomorph-rust_amd/lib/variants/libhm_$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "mul" > $OUT/pytest_$v.log 2>&1
+  HOMOMORPH_GPU_LIB=$PWD/homomorph-rust_amd/lib/variants/libhm_$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "${KEXPR:-mul}" > $OUT/pytest_$v.log 2>&1
   rc=$?; echo "[pytest $v] rc=$rc $(tail -n 1 $OUT/pytest_$v.log)"; [ $rc -eq 0 ] || exit $rc
 done
 for r in 1 2; do
