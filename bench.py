@@ -572,7 +572,7 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
 MIXED_PARAMS = (256, 256, 1, 256)  # BASELINE.json configs[4]: d = dp = tau = 256, delta = 1
 MIXED_CHUNK = 131072                # values per launch (the 8-GPU shard of 2^20)
 MUL_LOW_K = 8                       # result bits of the multiply half
-MIXED_KARATSUBA = (192, 192)        # hm_ctx_set_mul_options for the multiply half
+MIXED_KARATSUBA = (224, 224)        # hm_ctx_set_mul_options for the multiply half (scripts/sweep_mixed_ka.sh)
 
 
 def run_add(args, world, rank, device):
