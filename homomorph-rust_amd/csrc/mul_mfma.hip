@@ -26,7 +26,10 @@
 namespace hm {
 
 constexpr int kMfG = 16;      // chunks per full A group (64 VGPRs of A fragments)
-constexpr int kMfPf = 3;      // B reads issued ahead of their MFMA
+#ifndef HM_MF_PF
+#define HM_MF_PF 3
+#endif
+constexpr int kMfPf = HM_MF_PF; // B reads issued ahead of their MFMA
 constexpr int kVPad = 2 * kMfG + 32; // V words read beyond V's ends (zero)
 
 // U blocks of at most ub = min(umax, kMfUB) words: the launch's LDS slices are sized for them
@@ -107,7 +110,13 @@ __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI,
 }
 
 template <bool LEAF>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 3)))
+#ifndef HM_MF_WPE
+#define HM_MF_WPE 3
+#endif
+#ifndef HM_MF_WPE_MIN
+#define HM_MF_WPE_MIN 2
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HM_MF_WPE_MIN, HM_MF_WPE)))
 mul_mfma_kernel(MulMfmaArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
