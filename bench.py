@@ -128,11 +128,18 @@ def barrier(world):
         dist.barrier()
 
 
+def coll_device(device):
+    """Where a collective's tensors live: the rank's GPU under RCCL; the host under gloo (the CPU
+    tests, and the one-GPU rehearsal mode of setup_dist)."""
+    return torch.device("cpu") if dist.get_backend() == "gloo" else device
+
+
 def broadcast_keys(world, rank, device, sk=None, pk=None, params=PARAMS):
     """Rank 0's (sk, pk) limbs -> every rank (setup, untimed; RCCL on GPUs, gloo in the CPU
     tests).  Returns host uint64 arrays (sk: d/64+1 limbs, pk: tau x (d+dp)/64+1 limbs)."""
     if world == 1:
         return sk, pk
+    device = coll_device(device)
     d, dp, delta, tau = params
     skt = torch.zeros(d // 64 + 1, dtype=torch.int64, device=device)
     pkt = torch.zeros((tau, (d + dp) // 64 + 1), dtype=torch.int64, device=device)
@@ -177,6 +184,8 @@ def gather_results(world, device, res, wall):
     Returns (world*n x k numpy array in rank order, max wall time).  Identity at world 1."""
     if world == 1:
         return res.cpu().numpy(), float(wall)
+    device = coll_device(device)
+    res = res.to(device)
     parts = [torch.empty_like(res) for _ in range(world)]
     dist.all_gather(parts, res.contiguous())
     w = torch.tensor([float(wall)], dtype=torch.float64, device=device)
@@ -319,6 +328,23 @@ def hbm_roofline(alg_bytes, seconds, kernel, note):
             "frac": achieved / HBM_PEAK_GBS, "kernel": kernel, "note": note}
 
 
+def mfma_roofline(ops, seconds, kernel, note):
+    achieved = ops / seconds / 1e12
+    return {"bound": "mfma", "achieved": achieved, "peak": FP4_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP4_MFMA_PEAK_TFLOPS, "kernel": kernel, "note": note}
+
+
+def mul_roofline(word_pairs, n, seconds, what):
+    """MFMA roofline of a multiply (all of its launches): the carry-save circuit's algorithmic
+    bit pairs (hm_mul_cost word pairs x 1024, the planner's symbolic run of common.rs:66-105 over
+    the static bounds), 2 ops per pair, over the multiply's HIP-event time, vs the dense fp4 peak."""
+    return mfma_roofline(2.0 * 1024.0 * word_pairs * n, seconds,
+                         "mul_mfma_kernel + scan / partial-product / Karatsuba launches (whole multiply)",
+                         f"{what}: {word_pairs:.4g} word pairs (32x32 bit) per value from hm_mul_cost, "
+                         "2 ops per bit pair, over the multiply's HIP-event time on the engine "
+                         "stream (every launch of the multiply, not one kernel)")
+
+
 def s0_zero_context(device, params=PARAMS):
     """A seeded context whose secret key has S(0) = 0: (C mod S)(0) = C(0) and evaluation at 0 is a
     ring homomorphism, so every circuit output decrypts whatever its noise degree (DESIGN.md s6);
@@ -333,7 +359,89 @@ def s0_zero_context(device, params=PARAMS):
     raise RuntimeError("no S(0) = 0 seed")
 
 
-def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
+def config0_lines(device, leg_s):
+    """BASELINE.json configs[0]: the reference's `cargo bench --bench u8` plumbing (u8 encrypt,
+    decrypt and add at d = dp = tau = 64, delta = 1) -- on the GPU over a batch of 4096 u8 values,
+    each op one HIP graph replay per step, with the oracle's 1-thread rate of the same op beside
+    it."""
+    import ctypes
+    from oracle import oracle_py as oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import as_bytes, keys, masks
+    params = (64, 64, 1, 64)
+    L = H.lib()
+    c0 = H.Context(H.Parameters(*params), device=device)
+    c0.seed_rng(BENCH_SEED)
+    c0.generate_secret_key()
+    c0.generate_public_key()
+    n = 4096
+    a_np = np.random.default_rng(31).integers(0, 256, size=n, dtype=np.uint8)
+    b_np = np.random.default_rng(32).integers(0, 256, size=n, dtype=np.uint8)
+    da = torch.from_numpy(a_np).to(device).reshape(n, 1)
+    bound = np.full(8, c0.fresh_bound(), dtype=np.uint32)
+    ca = H.Ciphered.empty(n, bound, device)
+    cb = c0.encrypt(b_np)
+    dec = torch.empty((n, 1), dtype=torch.uint8, device=device)
+    cac = ca._c()
+    ob = H.add_out_bounds(bound, cb.bound)
+    co = H.Ciphered.empty(n, ob, device, np.dtype(np.uint8))
+    reps = 100
+
+    def timed(fn):
+        g = c0.graph(fn, warmup=2)
+        wall, ev_s = time_loop(g.replay, reps, 5, 1)
+        c0.synchronize()
+        return n * reps / wall, ev_s / reps
+
+    enc_r, enc_s = timed(lambda: c0._launch(lambda: L.hm_encrypt_batch(c0._h, da.data_ptr(), 1, None,
+                                                                       ctypes.byref(cac)), "encrypt"))
+    dec_r, dec_s = timed(lambda: c0._launch(lambda: L.hm_decrypt_batch(c0._h, ctypes.byref(cac),
+                                                                       dec.data_ptr()), "decrypt"))
+    dec_ok = bool(np.array_equal(dec.cpu().numpy().reshape(-1), a_np))
+    add_r, add_s = timed(lambda: H.add_into(c0, ca, cb, co))
+    got = c0.decrypt(co, np.uint8)
+    add_ok = int(np.sum(got == (a_np.astype(np.uint16) + b_np).astype(np.uint8)))
+    # the oracle on the same ops (its own seeded keys of the same parameters)
+    sk, pk, _ = keys(*params, 33)
+    ns = 64
+    ms = masks(ns, 8, params[3], 34)
+    la, lda = oracle.encrypt_batch(pk, as_bytes(a_np[:ns]), ms, bound)
+    lb, ldb = oracle.encrypt_batch(pk, as_bytes(b_np[:ns]), masks(ns, 8, params[3], 35), bound)
+    cpu_enc = oracle_leg(lambda: oracle.encrypt_batch(pk, as_bytes(a_np[:ns]), ms, bound), ns, leg_s,
+                         "u8 encryptions (64 per call)")
+    cpu_dec = oracle_leg(lambda: oracle.decrypt_batch(sk, la, lda, bound, 8, ns), ns, leg_s,
+                         "u8 decryptions of fresh ciphertexts (64 per call)")
+    cpu_add = oracle_leg(lambda: oracle.add_batch(la, lda, bound, lb, ldb, bound, 8, ns, ob), ns,
+                         leg_s, "u8 homomorphic adds (64 per call)")
+    cap = int(bound[0]) // 64 + 1
+    enc_b, dec_b = 8 * (8 * cap) + 8 * ((params[3] + 7) // 8), 8 * (8 * cap) + 1
+    add_b = 2 * 8 * (8 * cap) + 8 * co.stride
+    pairs = chain_bit_pairs(bound, cb.bound)
+    add_roof = mfma_roofline(2.0 * pairs * n, add_s, "add step (MFMA carry chain)",
+                             f"{pairs} carry-product bit pairs per u8 add (static bounds), 2 ops "
+                             "per pair, over the step's HIP-event time")
+    add_roof["hbm_frac"] = add_b * n / add_s / 1e9 / HBM_PEAK_GBS
+    out = {
+        "config0_u8_encrypt": {
+            "value": enc_r, "unit": "u8 encryptions/s", "batch": n, "params": params,
+            "kernel_us_per_step": 1e6 * enc_s, "masks": "drawn per step (engine CSPRNG)",
+            "roofline": hbm_roofline(enc_b * n, enc_s, "rand_fill_kernel + encrypt_table_kernel",
+                                     f"{enc_b} algorithmic B per u8: ciphertext written, masks read"),
+            "cpu_baseline": cpu_enc},
+        "config0_u8_decrypt": {
+            "value": dec_r, "unit": "u8 decryptions/s", "batch": n, "params": params,
+            "verified": dec_ok, "kernel_us_per_step": 1e6 * dec_s,
+            "roofline": hbm_roofline(dec_b * n, dec_s, "decrypt_bits_kernel",
+                                     f"{dec_b} algorithmic B per u8: ciphertext read, 1 B written"),
+            "cpu_baseline": cpu_dec},
+        "config0_u8_add": {
+            "value": add_r, "unit": "u8 homomorphic adds/s", "batch": n, "params": params,
+            "verified": {"correct_sums": add_ok, "of": n}, "kernel_us_per_step": 1e6 * add_s,
+            "roofline": add_roof, "cpu_baseline": cpu_add}}
+    del ca, cb, co, c0
+    return out
+
+def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     """The other BASELINE configs and the README's other published timings (README.md:73-77,
     benches/u32.rs:17-23, 47-49), each with the oracle's single-thread CPU rate beside it."""
     import ctypes
@@ -478,11 +586,17 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
         host["ol"].copy_(o4.limbs, non_blocking=True)
         host["od"].copy_(o4.degree, non_blocking=True)
 
-    wall, _ = time_loop(pcie_step, max(4, steps // 2), 1, 1)
+    preps = max(4, steps // 2)
+    wall, _ = time_loop(pcie_step, preps, 1, 1)
     moved = sum(v.numel() * v.element_size() for v in host.values())
-    out["u32_add_pcie_inclusive"] = {"value": n4 * max(4, steps // 2) / wall, "unit": "adds/s",
-                                     "batch": n4, "bytes_moved_per_step": moved,
-                                     "note": "H2D inputs + add + D2H outputs per step"}
+    out["u32_add_pcie_inclusive"] = {
+        "value": n4 * preps / wall, "unit": "adds/s", "batch": n4, "bytes_moved_per_step": moved,
+        "note": "H2D inputs + add + D2H outputs per step",
+        "roofline": hbm_roofline(moved * preps, wall, "H2D + add + D2H (wall time of the step)",
+                                 "the bytes crossing PCIe per step over the step's wall time vs "
+                                 "the HBM peak (the step is PCIe-bound: these bytes cross the host "
+                                 "link, not only HBM)"),
+        "cpu_baseline": cpu_add if cpu_add is not None else {"value": None, "note": "--no-cpu"}}
     del c4a, c4b, o4, host
 
     # Multiplies (configs[3]) under an S(0) = 0 key, so that every product's decryption is
@@ -495,12 +609,49 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
     co = H.Ciphered.empty(n8, H.mul_out_bounds(ca.bound, cbb.bound), device)
     H.mul_into(mctx, ca, cbb, co)  # sizes the workspace outside the timed loop
     mctx.synchronize()
-    wall, _ = time_loop(lambda: H.mul_into(mctx, ca, cbb, co), max(1, steps // 4), 1, 1)
+    mreps = max(1, steps // 4)
+    wall, ev_s = time_loop(lambda: H.mul_into(mctx, ca, cbb, co), mreps, 1, 1, mctx.stream)
     got = mctx.decrypt(co, np.uint8)
-    out["u8_mul"] = {"value": n8 * max(1, steps // 4) / wall, "unit": "u8 muls/s", "batch": n8,
+    # the oracle (1 thread) on the same workload: benches/u8.rs:9, 21-29 multiply u8 values at
+    # (128, 128, 1, 128); two values per call, the engine context's keys, seeded masks
+    msk, mpk = mctx.get_secret_key().limbs, mctx.get_public_key().limbs
+    b8b = ca.bound
+    o8a, o8ad = oracle.encrypt_batch(mpk, as_bytes(a8[:2]), hmasks(2, 8, PARAMS[3], 11), b8b)
+    o8b, o8bd = oracle.encrypt_batch(mpk, as_bytes(b8[:2]), hmasks(2, 8, PARAMS[3], 12), b8b)
+    ol8, od8 = oracle.mul_batch(o8a, o8ad, b8b, o8b, o8bd, b8b, 8, 2, co.bound)
+    cpu_m8 = oracle_leg(lambda: oracle.mul_batch(o8a, o8ad, b8b, o8b, o8bd, b8b, 8, 2, co.bound), 2,
+                        leg_s, "u8 homomorphic multiplies (2 per call; common.rs:66-105)")
+    w8 = H.mul_cost(ca.bound, cbb.bound, 8)["word_pairs"]
+    out["u8_mul"] = {"value": n8 * mreps / wall, "unit": "u8 muls/s", "batch": n8,
                      "verified": bool(np.array_equal(got, (a8.astype(int) * b8).astype(np.uint8))),
-                     "key_seed": mseed}
-    del ca, cbb, co
+                     "key_seed": mseed, "kernel_ms_per_batch": 1e3 * ev_s / mreps,
+                     "reference_bench": "benches/u8.rs:21-29 (mul at d=dp=tau=128, delta=1)",
+                     "roofline": mul_roofline(w8, n8, ev_s / mreps, "u8 multiply"),
+                     "cpu_baseline": cpu_m8}
+    # benches/u8.rs:31-37 "decipher after mul": decrypting the 1024 u8 products (the rem-heavy
+    # case of the multiply's wide outputs), one HIP graph replay per step
+    d8 = torch.empty((n8, 1), dtype=torch.uint8, device=device)
+    coc = co._c()
+    g8 = mctx.graph(lambda: mctx._launch(lambda: L.hm_decrypt_batch(mctx._h, ctypes.byref(coc),
+                                                                    d8.data_ptr()), "decrypt"),
+                    warmup=2)
+    dreps = max(20, 5 * steps)
+    wall, ev_s = time_loop(g8.replay, dreps, 2, 1)
+    mctx.synchronize()
+    per_u8 = 8 * co.stride + 1
+    cpu_d8 = oracle_leg(lambda: oracle.decrypt_batch(msk, ol8, od8, co.bound, 8, 2), 2, leg_s,
+                        "u8 decryptions of multiply outputs (2 per call; long division, "
+                        "polynomial.rs:316-365)")
+    out["u8_decrypt_after_mul"] = {
+        "value": n8 * dreps / wall, "unit": "u8 decryptions/s", "batch": n8,
+        "verified": bool(np.array_equal(d8.cpu().numpy().reshape(-1), got)),
+        "kernel_us_per_step": 1e6 * ev_s / dreps,
+        "reference_bench": "benches/u8.rs:31-37 (decipher after mul)",
+        "roofline": hbm_roofline(per_u8 * n8, ev_s / dreps, "decrypt_kernel (wave per value)",
+                                 f"{per_u8} algorithmic B per u8: the product at its static "
+                                 f"capacity read once, 1 B written"),
+        "cpu_baseline": cpu_d8}
+    del ca, cbb, co, d8, g8
 
     # SURVEY.md s8 row A14, configs[3] (u32 mul, batch 1024): the first K result bits of the u32
     # carry-save circuit, bit-exact (tests: oracle fixture at K = 16, residue checks of the full
@@ -509,6 +660,29 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
     a32 = np.random.default_rng(3).integers(0, 2**32, size=n8, dtype=np.uint32)
     b32 = np.random.default_rng(4).integers(0, 2**32, size=n8, dtype=np.uint32)
     c32a, c32b = mctx.encrypt(a32), mctx.encrypt(b32)
+    # the oracle's K = 12 circuit on one value (the low 12 bits of u32 ciphertexts, as the engine
+    # reads them); K >= 16 takes the oracle minutes to hours per value, so their CPU rates are this
+    # leg's word-pair rate applied to their word pairs (labelled extrapolated)
+    from helpers import low_bits
+    b32b = c32a.bound
+    o32a, o32ad = oracle.encrypt_batch(mpk, as_bytes(a32[:1]), hmasks(1, 32, PARAMS[3], 13), b32b)
+    o32b, o32bd = oracle.encrypt_batch(mpk, as_bytes(b32[:1]), hmasks(1, 32, PARAMS[3], 14), b32b)
+    l12a, d12a, bk12 = low_bits(o32a, o32ad, b32b, 1, 12)
+    l12b, d12b, _ = low_bits(o32b, o32bd, b32b, 1, 12)
+    ob12 = H.mul_out_bounds(bk12, bk12)
+    cpu_k12 = oracle_leg(lambda: oracle.mul_batch(l12a, d12a, bk12, l12b, d12b, bk12, 12, 1, ob12),
+                         1, leg_s, "u32 multiplies, result bits 0..11 (1 value per call; the "
+                                   "12-bit circuit over the low 12 input bits)")
+    k12_pairs_s = cpu_k12["value"] * H.mul_cost(b32b, b32b, 12)["word_pairs"]
+
+    def cpu_mul_low(k):
+        if k == 12:
+            return cpu_k12
+        wp = H.mul_cost(b32b, b32b, k)["word_pairs"]
+        return {"value": k12_pairs_s / wp, "cores": 1, "kind": "port", "cpu": cpu_model(),
+                "extrapolated": True,
+                "sample": f"EXTRAPOLATED: the K = 12 oracle leg's {k12_pairs_s:.3g} word pairs/s "
+                          f"(1 thread) applied to K = {k}'s {wp:.4g} word pairs (hm_mul_cost)"}
     for k, nk in ((12, n8), (MUL_LOW_BENCH, n8), (20, 16)):
         ob = H.mul_out_bounds(c32a.bound[:k], c32b.bound[:k])
         va, vb = H.value_slice(c32a, 0, nk), H.value_slice(c32b, 0, nk)
@@ -534,7 +708,9 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
             "word_pairs_per_s": cost["word_pairs"] * rate,
             "bit_exact": "tests/test_golden.py (K=16 oracle fixture, 8 values), "
                          "test_gpu_properties.py (residue check of all 1024 K=16 products; "
-                         "K=20 Karatsuba = schoolbook + residue check), test_gpu_parity.py"}
+                         "K=20 Karatsuba = schoolbook + residue check), test_gpu_parity.py",
+            "roofline": mul_roofline(cost["word_pairs"], nk, ev_s / reps, f"u32 multiply, low {k} bits"),
+            "cpu_baseline": cpu_mul_low(k)}
         del cp
     full = H.mul_cost(c32a.bound, c32b.bound)
     kx = out["u32_mul_low20"]
@@ -545,7 +721,13 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
                  "word pairs; the full circuit also needs its outputs and carries resident, "
                  "which no GPU holds",
         "word_pairs_per_mul": full["word_pairs"], "out_bytes_per_mul": full["out_bytes"],
-        "max_degree": full["max_degree"], "seconds_per_mul_one_gpu": 1.0 / est}
+        "max_degree": full["max_degree"], "seconds_per_mul_one_gpu": 1.0 / est,
+        "roofline": dict(kx["roofline"], note="EXTRAPOLATED: the low-20 multiply's measured "
+                         "roofline (the rate above is that word-pair rate)"),
+        "cpu_baseline": dict(cpu_mul_low(20), value=k12_pairs_s / full["word_pairs"],
+                             sample=f"EXTRAPOLATED: the K = 12 oracle leg's {k12_pairs_s:.3g} word "
+                                    f"pairs/s (1 thread) applied to the full circuit's "
+                                    f"{full['word_pairs']:.4g} word pairs")}
     del c32a, c32b, mctx
     torch.cuda.empty_cache()
 
@@ -556,6 +738,8 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
     wall, ev_s = time_loop(w.step, msteps, 1, 1, w.ctx.stream)
     w.ctx.synchronize()
     ok_s, ok_p, wall = w.verify(device, wall)
+    add_pairs = chain_bit_pairs(w.ca.bound, w.cb.bound)
+    mul_wp = H.mul_cost(w.ca.bound, w.cb.bound, MUL_LOW_K)["word_pairs"]
     out["mixed_config4"] = {
         "value": w.glob * msteps / wall,
         "unit": f"u32 values/s (one add + one mul, low {MUL_LOW_K} result bits, per value)",
@@ -563,10 +747,47 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds):
         "kernel_ms_per_step": 1e3 * ev_s / msteps,
         "config": {"d": MIXED_PARAMS[0], "dp": MIXED_PARAMS[1], "delta": MIXED_PARAMS[2],
                    "tau": MIXED_PARAMS[3], "launch_chunk": MIXED_CHUNK},
-        "verified": {"correct_sums": ok_s, "correct_products": ok_p, "of": w.glob}}
+        "verified": {"correct_sums": ok_s, "correct_products": ok_p, "of": w.glob},
+        "roofline": mfma_roofline(
+            2.0 * (add_pairs + 1024.0 * mul_wp) * w.glob, ev_s / msteps,
+            "add_chain_mfma_kernel<25> + the multiply's launches (whole step)",
+            f"per value: the add chain's {add_pairs:.4g} carry-product bit pairs (static bounds, "
+            f"DESIGN.md s4.1) + the low-{MUL_LOW_K} multiply's {mul_wp:.4g} word pairs x 1024 "
+            "(hm_mul_cost), 2 ops per bit pair, over the step's HIP-event time"),
+        "cpu_baseline": mixed_cpu_leg(leg_s)}
     del w
     torch.cuda.empty_cache()
+    out.update(config0_lines(device, leg_s))
     return out
+
+
+def mixed_cpu_leg(seconds):
+    """configs[4] on the oracle (1 thread): one u32 add and one u32 multiply (low MUL_LOW_K bits)
+    of one value per call at d = dp = tau = 256, timed on a sample and reported per value: the
+    2^20-value batch is extrapolated linearly (BASELINE.md:50)."""
+    from oracle import oracle_py as oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import as_bytes, fresh_bound, keys, low_bits, masks
+    d, dp, delta, tau = MIXED_PARAMS
+    _, pk, _ = keys(d, dp, delta, tau, 78)
+    bound = fresh_bound(d, dp, 32)
+    a = np.array([0x9E3779B9], dtype=np.uint32)
+    b = np.array([0x7F4A7C15], dtype=np.uint32)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), masks(1, 32, tau, 21), bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), masks(1, 32, tau, 22), bound)
+    ob = H.add_out_bounds(bound, bound)
+    lka, dka, bk = low_bits(la, da, bound, 1, MUL_LOW_K)
+    lkb, dkb, _ = low_bits(lb, db, bound, 1, MUL_LOW_K)
+    obk = H.mul_out_bounds(bk, bk)
+
+    def one():
+        oracle.add_batch(la, da, bound, lb, db, bound, 32, 1, ob)
+        oracle.mul_batch(lka, dka, bk, lkb, dkb, bk, MUL_LOW_K, 1, obk)
+
+    leg = oracle_leg(one, 1, seconds, f"values (one u32 add + one u32 multiply, low {MUL_LOW_K} "
+                                      "bits, at d = dp = tau = 256; 1 value per call)")
+    leg["extrapolated"] = "per-value rate of the sample; the 2^20 batch scales linearly (BASELINE.md:50)"
+    return leg
 
 
 MIXED_PARAMS = (256, 256, 1, 256)  # BASELINE.json configs[4]: d = dp = tau = 256, delta = 1
@@ -676,15 +897,16 @@ def run_add(args, world, rank, device):
                              "profiles/add_traffic.json (rocprofv3 --pmc passes of this bench "
                              "command), not measured in this run"},
     }
-    if rank == 0 and world == 1 and not args.no_secondary:
-        try:
-            # (the secondary lines' own repetition counts, independent of the headline's)
-            result["secondary"] = secondary_metrics(ctx, device, 10, out, args.cpu_seconds)
-        except Exception as e:  # reported, never fatal to the headline line
-            result["secondary"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline_add(args.cpu_seconds)
         result["verified"].update(confirm_noise(ctx, a, b, ca, cb, out, got[:n]))
+    if rank == 0 and world == 1 and not args.no_secondary:
+        try:
+            # (the secondary lines' own repetition counts, independent of the headline's)
+            result["secondary"] = secondary_metrics(ctx, device, 10, out, args.cpu_seconds,
+                                                    result.get("cpu_baseline"))
+        except Exception as e:  # reported, never fatal to the headline line
+            result["secondary"] = {"error": repr(e)}
     return result
 
 
@@ -813,7 +1035,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--add-chain", choices=["auto", "mfma", "valu"], default="auto",
+    ap.add_argument("--add-chain", choices=["auto", "mfma", "valu", "mfma_fused"], default="auto",
                     help="hm_ctx_set_add_options (auto = the MFMA chain where it applies)")
     ap.add_argument("--add-pipeline", type=int, default=0,
                     help="1: big adds run as two pipelined halves; 0: one pass (engine default)")

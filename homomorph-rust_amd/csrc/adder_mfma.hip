@@ -34,6 +34,7 @@
 // bit 0 of its f32 encoding is the coefficient.  One v_alignbit per accumulator gathers them.
 #include <hip/hip_runtime.h>
 
+#include "add_prep.h"
 #include "mfma_gf2.h"
 
 namespace hm {
@@ -118,14 +119,21 @@ static_assert(kMfmaWpb <= kAddWavesPerBlock, "host LDS plan");
 
 // NC = 13: 4 waves per SIMD (configs[1]'s 4096 waves fill the chip at that), 128 VGPRs;
 // NC = 25: 2 waves per SIMD, 256 VGPRs (the 25 A fragments alone are 100)
-template <int NC>
+//
+// FUSED: the wave also computes its own records (x_i, P_i, ab_i, degrees; add_prep.h
+// prep_records), A.fgrp bits at a time into LDS (A.fgrp records after RS), instead of reading the
+// workspace add_prep_kernel wrote: no prep launch before the chain, no workspace round trip
+// through HBM.  The bits' products are VALU work in a phase of their own, between two bits' tile
+// loops, where the tile loop's registers are dead; the other waves of the SIMD keep its matrix
+// core busy meanwhile.
+template <int NC, bool FUSED>
 __global__ void __launch_bounds__(64 * kMfmaWpb)
 __attribute__((amdgpu_waves_per_eu(MfmaCfg<NC>::kWavesPerEU, MfmaCfg<NC>::kWavesPerEU)))
 add_chain_mfma_kernel(AddArgs A) {
     using Cfg = MfmaCfg<NC>;
     constexpr int kRevWords = Cfg::kRevWords, kRsWords = Cfg::kRsWords, kRec = Cfg::kRecWords;
     extern __shared__ uint32_t lds[];
-    __shared__ uint32_t stage[kMfmaWpb][2][kRec];
+    __shared__ uint32_t stage[FUSED ? 1 : kMfmaWpb][2][FUSED ? 1 : kRec];
     uint32_t *tab = lds; // byte -> 8 nibbles, fp4 1.0 (0b0010) per set bit
     for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
         uint32_t v = 0u;
@@ -139,12 +147,13 @@ add_chain_mfma_kernel(AddArgs A) {
     if (e >= A.n) return; // whole wave exits together
     const int lane = lane_id();
     const uint32_t L = A.nbits;
-    // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][RS: kRsWords]
+    // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][RS: kRsWords][FUSED: fgrp records]
     uint32_t *Ls = lds + 256 + (size_t)wave * A.chain_lds;
     uint32_t *C = Ls + Cfg::kHalo;
     uint32_t *ring = C + A.mf_cw;
     uint32_t *RS = ring + 8 * kMfmaRingSlots;
-    const uint32_t *ws = A.ws + e * A.ws_stride;
+    uint32_t *recs = RS + kRsWords;
+    const uint32_t *ws = FUSED ? nullptr : A.ws + e * A.ws_stride;
     uint64_t *po = A.out.limbs + e * A.out.stride;
     uint32_t *dout = A.out.degree + e * L;
     // Bit i's workspace record, copied into stage[wave][i&1] by one LDS-DMA a bit ahead (its
@@ -170,6 +179,7 @@ add_chain_mfma_kernel(AddArgs A) {
     const uint64_t wsu = ((uint64_t)rfl((uint32_t)((uintptr_t)ws >> 32)) << 32) |
                          rfl((uint32_t)(uintptr_t)ws); // wave-uniform: SGPR base of the DMA
     auto stage_rec = [&](uint32_t i) {
+        if constexpr (FUSED) return;
         const uint32_t voff = 4u * (lbase + i * lstep);
         const uint32_t m0 = (uint32_t)(uintptr_t)&stage[wave][i & 1][0]; // LDS byte offset
         asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
@@ -196,10 +206,25 @@ add_chain_mfma_kernel(AddArgs A) {
     int degc = -1; // the carry's degree
     int tw = -1;   // > 0: the previous bit's tiles stored sum words [cntX, min(tw, cap words))
     uint32_t offo = 0;
+    const uint32_t recw = A.recw;
+    uint32_t gbase = 0; // FUSED: the bit of recs[0]
     for (uint32_t i = 0; i < L; ++i) {
         HM_PT(tw0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
-        const uint32_t *rec = &stage[wave][i & 1][0];
+        const uint32_t *rec;
+        if constexpr (FUSED) {
+            if (i == 0 || i - gbase == A.fgrp) { // the next group's records (RS is free here)
+                gbase = i;
+                wsync();
+                prep_records(A, e, i, min(A.fgrp, L - i), recs, recw, RS);
+                // the scratch overwrote RS's zero tail (nibble words past P's image)
+                for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u;
+                wsync();
+            }
+            rec = recs + (i - gbase) * recw;
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
+            rec = &stage[wave][i & 1][0];
+        }
         // s_i = x_i ^ carry_i (common.rs:43-47)
         HM_PT(t0);
         HM_PACC(3, tw0, t0);
@@ -373,14 +398,19 @@ int launch_add_chain_mfma(const AddArgs &a, void *stream) {
     const int wpb = kMfmaWpb;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     const size_t lds = (256 + (size_t)a.chain_lds * wpb) * 4;
-    if (a.mfma == MfmaCfg<13>::kChunks)
-        hipLaunchKernelGGL(add_chain_mfma_kernel<13>, dim3((unsigned)blocks), dim3(64 * wpb), lds,
-                           (hipStream_t)stream, a);
-    else if (a.mfma == MfmaCfg<25>::kChunks)
-        hipLaunchKernelGGL(add_chain_mfma_kernel<25>, dim3((unsigned)blocks), dim3(64 * wpb), lds,
-                           (hipStream_t)stream, a);
-    else
+#define HM_LAUNCH_CHAIN(NCV, F)                                                                   \
+    hipLaunchKernelGGL((add_chain_mfma_kernel<NCV, F>), dim3((unsigned)blocks), dim3(64 * wpb), \
+                       lds, (hipStream_t)stream, a)
+    if (a.mfma == MfmaCfg<13>::kChunks) {
+        if (a.fgrp) HM_LAUNCH_CHAIN(13, true);
+        else HM_LAUNCH_CHAIN(13, false);
+    } else if (a.mfma == MfmaCfg<25>::kChunks) {
+        if (a.fgrp) HM_LAUNCH_CHAIN(25, true);
+        else HM_LAUNCH_CHAIN(25, false);
+    } else {
         return -1;
+    }
+#undef HM_LAUNCH_CHAIN
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

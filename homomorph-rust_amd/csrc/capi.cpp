@@ -84,6 +84,18 @@ std::vector<uint64_t> clmul_host(const std::vector<uint64_t> &a, const std::vect
     return r;
 }
 
+// 64x64 bit-matrix transpose in place: bit j of m[u] moves to bit u of m[j] (block swaps of
+// halving size; the remainder table's columns are built as rows of X^k mod S)
+void transpose64(uint64_t m[64]) {
+    uint64_t mask = 0x00000000FFFFFFFFull;
+    for (unsigned s = 32; s; s >>= 1, mask ^= mask << s)
+        for (unsigned u = 0; u < 64; u = ((u | s) + 1) & ~s) {
+            const uint64_t x = ((m[u] >> s) ^ m[u | s]) & mask;
+            m[u] ^= x << s;
+            m[u | s] ^= x;
+        }
+}
+
 uint16_t min_d_over_delta(hm_op op) { // src/impls/numbers.rs:27-50
     switch (op) {
     case HM_OP_AND: case HM_OP_OR: return 2;
@@ -252,6 +264,11 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         cus = 256;
     c->cus = (uint32_t)std::max(cus, 1);
+    // fp4 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4) is a gfx950 instruction: AUTO strategies use
+    // the matrix cores only there, and an explicit MFMA request elsewhere is HM_ERR_UNSUPPORTED
+    hipDeviceProp_t prop{};
+    c->fp4_mfma = hipGetDeviceProperties(&prop, device) == hipSuccess &&
+                  std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
     *out = c;
     return HM_OK;
 }
@@ -442,7 +459,7 @@ hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) 
 }
 
 hm_status hm_ctx_set_add_options(hm_ctx *c, uint32_t chain) {
-    if (!c || chain > HM_ADD_CHAIN_VALU) return HM_ERR_INVALID_ARGUMENT;
+    if (!c || chain > HM_ADD_CHAIN_MFMA_FUSED) return HM_ERR_INVALID_ARGUMENT;
     c->add_chain = chain;
     return HM_OK;
 }
@@ -462,6 +479,7 @@ hm_status hm_ctx_set_add_pipeline(hm_ctx *c, int enable) {
 
 hm_status hm_ctx_set_mul_products(hm_ctx *c, uint32_t products) {
     if (!c || products > HM_MUL_PRODUCTS_VALU) return HM_ERR_INVALID_ARGUMENT;
+    if (products == HM_MUL_PRODUCTS_MFMA && !c->fp4_mfma) return HM_ERR_UNSUPPORTED;
     c->mul_products = products;
     return HM_OK;
 }
@@ -716,18 +734,38 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
                                   160 * 1024;
             return fits ? lds : 0u;
         };
-        uint32_t nc = 0, lds = 0;
-        if ((lds = plan(MfmaCfg<13>{}))) nc = 13;
-        else if ((lds = plan(MfmaCfg<25>{}))) nc = 25;
+        uint32_t nc = 0, lds = 0, rs = 0, wpe = 0;
+        if ((lds = plan(MfmaCfg<13>{}))) nc = 13, rs = MfmaCfg<13>::kRsWords, wpe = MfmaCfg<13>::kWavesPerEU;
+        else if ((lds = plan(MfmaCfg<25>{}))) nc = 25, rs = MfmaCfg<25>::kRsWords, wpe = MfmaCfg<25>::kWavesPerEU;
+        if (!c->fp4_mfma) nc = 0;
         A.mfma = c->add_chain != HM_ADD_CHAIN_VALU ? nc : 0u;
-        if (c->add_chain == HM_ADD_CHAIN_MFMA && !nc) return HM_ERR_UNSUPPORTED;
+        if ((c->add_chain == HM_ADD_CHAIN_MFMA || c->add_chain == HM_ADD_CHAIN_MFMA_FUSED) && !nc)
+            return HM_ERR_UNSUPPORTED;
         if (A.mfma) A.mf_cw = mf_cw, A.chain_lds = lds;
+        // Fused prep (adder_mfma.hip FUSED): the chain's wave computes its records fgrp bits at a
+        // time into LDS after RS.  The largest group whose rows fit one pass of 64 lanes, whose
+        // staged inputs fit the RS scratch, and whose records leave the chain its full occupancy
+        // (kWavesPerEU blocks of 4 waves per CU); none fits -> the separate prep launch.
+        if (A.mfma && c->add_chain == HM_ADD_CHAIN_MFMA_FUSED && !c->add_pipe) {
+            const uint32_t recw = even(cntX + cntP + cntAB + 2);
+            for (uint32_t g = std::min<uint32_t>(L, std::max<uint32_t>(1, 64 / cntX)); g >= 1; --g) {
+                const uint32_t wl = lds + g * recw;
+                const size_t block = (256 + (size_t)wl * kAddWavesPerBlock) * 4 + 8;
+                if (g * (cntA + cntB + 2) <= rs && block <= (size_t)160 * 1024 / wpe) {
+                    A.fgrp = g, A.recw = recw, A.chain_lds = wl;
+                    break;
+                }
+            }
+            if (!A.fgrp) return HM_ERR_UNSUPPORTED;
+        }
     }
-    A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
-    const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
     DeviceGuard g(c->device);
-    HM_HIP(c, grow(c, c->d_ws_add, c->ws_add_bytes, bytes));
-    A.ws = c->d_ws_add;
+    if (!A.fgrp) { // the prep launch's workspace (the fused chain keeps its records in LDS)
+        A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
+        const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
+        HM_HIP(c, grow(c, c->d_ws_add, c->ws_add_bytes, bytes));
+        A.ws = c->d_ws_add;
+    }
     A.a = batch_arg(a), A.b = batch_arg(b), A.out = batch_arg(out);
     A.n = a->n, A.nbits = L;
     A.status = c->d_status;
@@ -747,10 +785,19 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     // halves use disjoint workspace and outputs.  Fork / join by events, so a graph captured on
     // the context stream holds both branches.
     if (c->add_pipe && !c->time_chain && A.mfma && a->n >= 2 * kAddPipeMin) {
-        if (!c->aux_stream) {
-            HM_HIP(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-            for (hipEvent_t *e : {&c->ev_fork, &c->ev_mid, &c->ev_join})
-                HM_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+        if (!c->aux_stream) { // created into locals, stored only when all of them exist
+            hipStream_t s = nullptr;
+            hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+            hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            for (int k = 0; k < 3 && e == hipSuccess; ++k)
+                e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+            if (e != hipSuccess) {
+                for (hipEvent_t x : ev)
+                    if (x) (void)hipEventDestroy(x);
+                if (s) (void)hipStreamDestroy(s);
+                return hip_fail(c, e);
+            }
+            c->aux_stream = s, c->ev_fork = ev[0], c->ev_mid = ev[1], c->ev_join = ev[2];
         }
         const uint64_t h = (a->n / 2 + kAddWavesPerBlock - 1) / kAddWavesPerBlock * kAddWavesPerBlock;
         const AddArgs A1 = add_args_slice(A, 0, h), A2 = add_args_slice(A, h, a->n - h);
@@ -870,31 +917,61 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
     if (!nz) return HM_ERR_DIVIDE_BY_ZERO;           // polynomial.rs:319-322
     const size_t ds = degree_of(s, sn);
     if (ds == 0) return HM_ERR_DIVISOR_IS_ONE;       // the reference never terminates
-    if (a->cap > 512) return HM_ERR_UNSUPPORTED;     // poly_rem_kernel: 8 limbs per lane
-    // remainder table: row j, bit k = bit j of X^k mod S, for k < 64 * a->cap
-    const size_t sl = ds / 64 + 1, acap = a->cap;
-    std::vector<uint64_t> zt(ds * acap, 0), r(sl, 0);
-    r[0] = 1; // X^0 mod S (deg S >= 1)
-    for (size_t k = 0; k < 64 * acap; ++k) {
-        for (size_t j = 0; j < ds; ++j)
-            if ((r[j / 64] >> (j % 64)) & 1) zt[j * acap + k / 64] |= 1ull << (k % 64);
-        uint64_t carry = 0; // r = X * r mod S
-        for (size_t w = 0; w < sl; ++w) {
-            const uint64_t nc = r[w] >> 63;
-            r[w] = (r[w] << 1) | carry;
-            carry = nc;
-        }
-        if ((r[ds / 64] >> (ds % 64)) & 1)
-            for (size_t w = 0; w < sl; ++w) r[w] ^= s[w];
-    }
     DeviceGuard g(c->device);
-    size_t have = c->d_s_limbs * 8;
-    HM_HIP(c, grow(c, c->d_s, have, zt.size() * 8));
-    c->d_s_limbs = have / 8;
-    HM_HIP(c, hipMemcpyAsync(c->d_s, zt.data(), zt.size() * 8, hipMemcpyHostToDevice, c->stream));
-    HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer is released after return
-    const int rc = launch_poly_rem(poly_args(c, a, nullptr, out), c->d_s, (uint32_t)ds, c->stream);
-    if (rc == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
+    const size_t acap = a->cap, kmax = 64 * acap;
+    RemTable T{nullptr, 0, 0, 0};
+    if (ds < kmax) {
+        // Remainder table (poly_rem_kernel): row j < deg S, bit k = bit j of X^k mod S.  Columns
+        // k < deg S are the identity (X^k mod S = X^k), so rows hold only the limbs from
+        // l0 = deg S / 64 on; size and build time are bounded by the dividend's capacity whatever
+        // the divisor's degree (a divisor above every dividend needs no table: zt = null).
+        const size_t l0 = ds / 64, tcols = acap - l0, sl = ds / 64 + 1;
+        if ((double)ds * tcols * 8 > 4.0 * (1ull << 30)) return HM_ERR_UNSUPPORTED; // host memory
+        std::vector<uint64_t> zt(ds * tcols, 0);
+        // X^k mod S for the 64 k of column limb l0 + t: unit bits below deg S, then r = X * r mod
+        // S; each block of 64 vectors is transposed word by word into the rows
+        std::vector<uint64_t> r(sl, 0), blk(64 * sl);
+        bool iter = false;
+        for (size_t t = 0; t < tcols; ++t) {
+            for (size_t u = 0; u < 64; ++u) {
+                const size_t k = 64 * (l0 + t) + u;
+                uint64_t *v = &blk[u * sl];
+                if (k < ds) {
+                    std::fill(v, v + sl, 0ull);
+                    v[k / 64] = 1ull << (k % 64);
+                    continue;
+                }
+                if (!iter) { // X^ds mod S = S - X^ds
+                    std::copy(s, s + sl, r.begin());
+                    r[ds / 64] &= ~(1ull << (ds % 64));
+                    iter = true;
+                } else {
+                    uint64_t carry = 0;
+                    for (size_t w = 0; w < sl; ++w) {
+                        const uint64_t nc = r[w] >> 63;
+                        r[w] = (r[w] << 1) | carry;
+                        carry = nc;
+                    }
+                    if ((r[ds / 64] >> (ds % 64)) & 1)
+                        for (size_t w = 0; w < sl; ++w) r[w] ^= s[w];
+                }
+                std::copy(r.begin(), r.end(), v);
+            }
+            uint64_t m[64];
+            for (size_t w = 0; w < sl; ++w) {
+                for (size_t u = 0; u < 64; ++u) m[u] = blk[u * sl + w];
+                transpose64(m); // m[jb] bit u = bit jb of word w of X^(64(l0+t)+u) mod S
+                for (size_t jb = 0; jb < 64 && 64 * w + jb < ds; ++jb) zt[(64 * w + jb) * tcols + t] = m[jb];
+            }
+        }
+        size_t have = c->d_s_limbs * 8;
+        HM_HIP(c, grow(c, c->d_s, have, zt.size() * 8));
+        c->d_s_limbs = have / 8;
+        HM_HIP(c, hipMemcpyAsync(c->d_s, zt.data(), zt.size() * 8, hipMemcpyHostToDevice, c->stream));
+        HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer is released after return
+        T = RemTable{c->d_s, (uint32_t)ds, (uint32_t)l0, (uint32_t)tcols};
+    }
+    const int rc = launch_poly_rem(poly_args(c, a, nullptr, out), T, c->stream);
     return rc ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
 

@@ -93,7 +93,7 @@ template <int PC>
 __device__ __forceinline__ void enc_lookup2(uint32_t *acc, const uint4 *tab4, uint32_t g,
                                             uint32_t nib0, uint32_t nib1) {
     constexpr int NP = (PC + 1) / 2;
-    const uint4 *r0 = tab4 + (size_t)g * NP * 16 + nib0, *r1 = r0 + NP * 16 + (nib1 - nib0);
+    const uint4 *r0 = tab4 + (size_t)g * NP * 16 + nib0, *r1 = tab4 + (size_t)(g + 1) * NP * 16 + nib1;
 #pragma unroll
     for (int p = 0; p < PC / 2; ++p) {
         const uint4 a = r0[p * 16], b = r1[p * 16];

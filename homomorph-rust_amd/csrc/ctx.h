@@ -47,6 +47,7 @@ struct hm_ctx {
     size_t masks_bytes = 0;
     int *d_status = nullptr;
     uint32_t cus = 256;                // compute units of the device (grid sizing)
+    bool fp4_mfma = false;             // the device has the gfx950 fp4 MFMA (set at creation)
     hipError_t last_hip = hipSuccess;
     // Device buffers the kernels read are never freed while the context lives: a HIP graph
     // captured over the engine's launches holds their raw pointers.  A buffer that has to be
@@ -97,6 +98,12 @@ struct DeviceGuard {
 };
 
 inline uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
+
+// hm_ctx_set_mul_products: MFMA, or AUTO on a device with the fp4 MFMA (gfx950)
+inline bool mul_on_mfma(const hm_ctx *c) {
+    return c->mul_products == HM_MUL_PRODUCTS_MFMA ||
+           (c->mul_products == HM_MUL_PRODUCTS_AUTO && c->fp4_mfma);
+}
 inline uint32_t words_of_bound(int64_t b) { return b < 0 ? 0u : (uint32_t)(b / 32 + 1); }
 
 inline void retire(hm_ctx *c, void *p, size_t bytes, bool secret) {

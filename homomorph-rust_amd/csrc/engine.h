@@ -43,6 +43,9 @@ struct AddArgs {
     uint32_t mfma;                    // chain on the matrix cores (adder_mfma.hip): its chunk count
                                       // NC (MfmaCfg), 0 = the VALU chain
     uint32_t mf_cw;                   // MFMA chain: carry bit words (tiles, window overhang)
+    uint32_t fgrp;                    // MFMA chain: > 0 = fused (no prep launch): bits per group
+                                      // whose records the chain's wave computes itself
+    uint32_t recw;                    // fused: words per LDS record (x, P, ab, two degrees)
     int *status;
     Bounds ab, bb, ob;
 };
@@ -262,8 +265,14 @@ int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches
 int launch_poly_add(const PolyArgs &a, void *stream);
 int launch_poly_mul(const PolyArgs &a, void *stream);
-// zt: the remainder table (kernels.hip poly_rem_kernel), s_deg rows of a.acap limbs
-int launch_poly_rem(const PolyArgs &a, const uint64_t *zt, uint32_t s_deg, void *stream);
+// The remainder table of poly_rem_kernel (kernels.hip): rows j < deg S of tcols limbs, row j's
+// limb t = bits 64 (l0 + t) .. of Z_j (bit k = bit j of X^k mod S); zt = null: deg S is above
+// every dividend (the remainder is the dividend)
+struct RemTable {
+    const uint64_t *zt;
+    uint32_t rows, l0, tcols;
+};
+int launch_poly_rem(const PolyArgs &a, const RemTable &t, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
 constexpr uint64_t kAddPipeMin = 1024; // values per half of a pipelined add (hm_ctx_set_add_pipeline)

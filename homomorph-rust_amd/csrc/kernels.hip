@@ -110,41 +110,54 @@ __global__ void __launch_bounds__(256) poly_mul_kernel(PolyArgs P) {
 
 // Remainder by one divisor S (polynomial.rs:316-365) as a table remainder:
 // C mod S = XOR over the set bits k of C of (X^k mod S), so remainder bit j is the parity of
-// C AND Z_j, where bit k of the row Z_j is bit j of X^k mod S (zt: sdeg rows of acap limbs, built
-// by the host).  The same linear functional as the decrypt table (row j = 0), for every bit of
-// the remainder; identical to the long division's remainder, which is unique.  One wave per
-// polynomial: lanes hold C's limbs, one ballot per remainder bit gives its parity.
-constexpr int kRemLimbsPerLane = 8; // polynomials up to 512 limbs (32768 coefficients)
+// C AND Z_j, where bit k of the row Z_j is bit j of X^k mod S.  The same linear functional as the
+// decrypt table (row j = 0), for every bit of the remainder; identical to the long division's
+// remainder, which is unique.  For k < deg S, X^k mod S = X^k: those columns are the identity, so
+// the host table (zt, built in hm_poly_rem_batch) holds rows j < deg S over the limbs from
+// l0 = deg S / 64 on only (tcols = acap - l0 limbs per row), and remainder word w < l0 starts as
+// C's limb w.  zt = null: the divisor is above every dividend's degree, the remainder is C.
+// One wave per polynomial: lanes hold C's first 512 limbs in registers (limbs past them are
+// re-read from memory for every row, so any dividend size is accepted, as polynomial.rs:316-365
+// accepts it), one ballot per remainder bit gives its parity.
+constexpr int kRemLimbsPerLane = 8; // limbs held in registers: 512 (32768 coefficients)
 
-__global__ void __launch_bounds__(256) poly_rem_kernel(PolyArgs P, const uint64_t *zt, uint32_t sdeg) {
+__global__ void __launch_bounds__(256) poly_rem_kernel(PolyArgs P, RemTable T) {
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
     if (e >= P.n) return;
     const int lane = lane_id();
     const uint64_t *a = P.a + e * P.acap;
     uint64_t *r = P.out + e * P.ocap;
-    const int na = poly_words(a, rfl(P.adeg[e])) ? (int)(rfl(P.adeg[e]) / 64 + 1) : 0;
+    const uint32_t adeg = rfl(P.adeg[e]);
+    const int na = poly_words(a, adeg) ? (int)(adeg / 64 + 1) : 0;
+    if (!T.zt) { // deg S above every dividend: C mod S = C
+        for (int k = lane; k < (int)P.ocap; k += kWave) r[k] = k < na ? a[k] : 0ull;
+        if (lane == 0) P.odeg[e] = na ? adeg : 0u;
+        return;
+    }
+    const int l0 = (int)T.l0;
     uint64_t c[kRemLimbsPerLane];
 #pragma unroll
     for (int t = 0; t < kRemLimbsPerLane; ++t) {
         const int k = lane + kWave * t;
-        c[t] = k < na ? a[k] : 0ull;
+        c[t] = k >= l0 && k < na ? a[k] : 0ull;
     }
-    // remainder bits, 64 at a time: lane j%64 keeps word j/64's bit j%64
-    // remainder limbs: degree < sdeg, and < 64 acap (a remainder never exceeds its dividend)
-    const int rl = min((int)(sdeg + 63) / 64, (int)P.ocap);
+    // remainder bits, 64 at a time: lane j%64 keeps word j/64's bit j%64; degree < deg S
+    const int rl = min((int)(T.rows + 63) / 64, (int)P.ocap);
     int top = -1;
     for (int w = 0; w < rl; ++w) {
-        uint64_t word = 0ull;
-        for (int jb = 0; jb < 64 && 64 * w + jb < (int)sdeg; ++jb) {
-            const uint64_t *z = zt + (size_t)(64 * w + jb) * P.acap;
+        uint64_t word = w < l0 && w < na ? a[w] : 0ull; // the identity columns (wave-uniform)
+        for (int jb = 0; jb < 64 && 64 * w + jb < (int)T.rows; ++jb) {
+            const uint64_t *z = T.zt + (size_t)(64 * w + jb) * T.tcols - l0; // z[k], k >= l0
             uint32_t par = 0u;
 #pragma unroll
             for (int t = 0; t < kRemLimbsPerLane; ++t) {
                 const int k = lane + kWave * t;
-                if (k < na) par ^= (uint32_t)__popcll(c[t] & z[k]);
+                if (k >= l0 && k < na) par ^= (uint32_t)__popcll(c[t] & z[k]);
             }
+            for (int k = max(kWave * kRemLimbsPerLane, l0) + lane; k < na; k += kWave)
+                par ^= (uint32_t)__popcll(a[k] & z[k]);
             const uint64_t m = __ballot(par & 1u);
-            word |= (uint64_t)(__popcll(m) & 1) << jb;
+            word ^= (uint64_t)(__popcll(m) & 1) << jb;
         }
         if (lane == 0) r[w] = word; // word is wave-uniform
         if (word) top = 64 * w + 63 - __builtin_clzll(word);
@@ -165,11 +178,10 @@ int launch_poly_mul(const PolyArgs &P, void *stream) {
                        (hipStream_t)stream, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_poly_rem(const PolyArgs &P, const uint64_t *zt, uint32_t sdeg, void *stream) {
+int launch_poly_rem(const PolyArgs &P, const RemTable &T, void *stream) {
     if (!P.n) return 0;
-    if (P.acap > (uint32_t)(kWave * kRemLimbsPerLane)) return HM_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(poly_rem_kernel, dim3((unsigned)((P.n + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, P, zt, sdeg);
+                       (hipStream_t)stream, P, T);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

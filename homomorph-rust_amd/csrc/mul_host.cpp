@@ -430,7 +430,7 @@ hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const 
                    bool is_signed, MulPlan *&out) {
     for (MulPlan *p : c->mul_plans)
         if (p->L == L && p->K == K && p->is_signed == is_signed && p->ka_min == c->ka_min &&
-            p->ka_leaf == c->ka_leaf && p->mfma == (c->mul_products != HM_MUL_PRODUCTS_VALU) &&
+            p->ka_leaf == c->ka_leaf && p->mfma == mul_on_mfma(c) &&
             std::equal(p->ab.begin(), p->ab.end(), ab) && std::equal(p->bb.begin(), p->bb.end(), bb)) {
             out = p;
             return HM_OK;
@@ -438,7 +438,7 @@ hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const 
     auto P = std::make_unique<MulPlan>();
     P->L = L, P->K = K, P->is_signed = is_signed;
     P->ka_min = c->ka_min, P->ka_leaf = c->ka_leaf;
-    P->mfma = c->mul_products != HM_MUL_PRODUCTS_VALU;
+    P->mfma = mul_on_mfma(c);
     P->ab.assign(ab, ab + K), P->bb.assign(bb, bb + K);
     if (!build_plan(*P)) return HM_ERR_UNSUPPORTED;
     if (hm_status st = upload_plan(c, *P); st) {
@@ -514,7 +514,7 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         a.B = B, a.t = (const KaSum *)(T + P.off_ka_sums) + lv[0], a.nt = lv[1], a.h = lv[2];
         if (launch_ka_sum(a, c->stream)) return hip_fail(c, hipGetLastError());
     }
-    if (c->mul_products != HM_MUL_PRODUCTS_VALU) {
+    if (P.mfma) {
         // the leaves on the matrix cores: one wave per (value, leaf)
         MulMfmaArgs a{};
         a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;

@@ -428,7 +428,7 @@ class Context:
                               "(run more warm-up calls)")
         return EngineGraph(self, g, gen)
 
-    ADD_CHAINS = {"auto": 0, "mfma": 1, "valu": 2}
+    ADD_CHAINS = {"auto": 0, "mfma": 1, "valu": 2, "mfma_fused": 3}
 
     def set_add_options(self, chain: str = "auto"):
         """hm_ctx_set_add_options: where the adder's carry products run -- "mfma" (fp4 matrix
@@ -467,9 +467,13 @@ class Context:
     MUL_PRODUCTS = {"auto": 0, "mfma": 1, "valu": 2}
 
     def set_mul_products(self, products: str = "auto"):
-        """hm_ctx_set_mul_products: where the multiplier's Karatsuba leaf products run -- "mfma"
-        (fp4 matrix cores, {0,1} Toeplitz GEMMs reduced mod 2; the default, "auto") or "valu"
-        (scalar-decided XORs).  Results are identical either way (every product is exact)."""
+        """hm_ctx_set_mul_products: where the multiplier's products run -- "mfma" (fp4 matrix
+        cores, {0,1} Toeplitz GEMMs reduced mod 2) or "valu".  It covers every product kind of
+        the carry-save plan: Karatsuba leaves, schoolbook carry products and the partial products
+        of fresh operands (operands below 4 words and the signed circuit's flipped partial
+        products stay on the VALU).  "auto" (the default) = MFMA on a gfx950 device, VALU
+        elsewhere; "mfma" without the fp4 MFMA raises EngineError (HM_ERR_UNSUPPORTED).  Results
+        are identical either way (every product is exact)."""
         _check(lib().hm_ctx_set_mul_products(self._h, self.MUL_PRODUCTS[products]),
                "hm_ctx_set_mul_products")
 

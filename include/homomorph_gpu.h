@@ -157,9 +157,13 @@ hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
 hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
                                  uint32_t karatsuba_leaf_words);
 
-/* Where the multiplier's Karatsuba leaf products run (no effect on results: every product is
- * exact): as {0,1} Toeplitz GEMMs on the fp4 matrix cores (MFMA, reduced mod 2) or as
- * scalar-decided VALU XORs.  AUTO = MFMA. */
+/* Where the multiplier's products run (no effect on results: every product is exact): as {0,1}
+ * Toeplitz GEMMs on the fp4 matrix cores (MFMA, reduced mod 2) or as VALU products.  The choice
+ * covers every product kind of the carry-save plan: the Karatsuba leaf products, the schoolbook
+ * carry products p_t * x_t, and the partial products a_j * b_k of fresh operands (products whose
+ * shorter operand is below 4 words, and the signed circuit's flipped partial products, stay on
+ * the VALU either way).  AUTO = MFMA on a device with the gfx950 fp4 MFMA, VALU elsewhere;
+ * MFMA on a device without it is HM_ERR_UNSUPPORTED. */
 #define HM_MUL_PRODUCTS_AUTO 0u
 #define HM_MUL_PRODUCTS_MFMA 1u
 #define HM_MUL_PRODUCTS_VALU 2u
@@ -169,10 +173,16 @@ hm_status hm_ctx_set_mul_products(hm_ctx *ctx, uint32_t products);
  * carry' = ab_i ^ P_i * carry (src/impls/numbers/common.rs:37-56) runs its products either on the
  * matrix cores (a {0,1} Toeplitz product on fp4 MFMA, reduced mod 2; needs P_i within 49 words,
  * i.e. d + dp <= 512 for u32) or as scalar-decided VALU XORs.  AUTO picks the MFMA chain when it
- * applies; MFMA on a plan it cannot run returns HM_ERR_UNSUPPORTED at hm_add_batch. */
+ * applies (and the device has the gfx950 fp4 MFMA); MFMA on a plan or device it cannot run
+ * returns HM_ERR_UNSUPPORTED at hm_add_batch. */
 #define HM_ADD_CHAIN_AUTO 0u
 #define HM_ADD_CHAIN_MFMA 1u
 #define HM_ADD_CHAIN_VALU 2u
+/* The MFMA chain computing its carry-independent products (ab_i, P_i) in the chain kernel's own
+ * waves, a group of bits at a time into LDS, instead of a separate prep launch writing an HBM
+ * workspace (AUTO and MFMA).  Same results; HM_ERR_UNSUPPORTED where the records do not fit the
+ * chain's LDS at full occupancy. */
+#define HM_ADD_CHAIN_MFMA_FUSED 3u
 hm_status hm_ctx_set_add_options(hm_ctx *ctx, uint32_t chain);
 
 /* Adder pipelining (no effect on results; off by default: measured no faster on configs[1],

@@ -74,7 +74,13 @@ def test_poly_mul_add(H, oracle, ca, cb):
 
 
 @pytest.mark.parametrize("cap,sdeg", [(1, 1), (3, 128), (20, 128), (9, 63), (9, 64), (50, 700),
-                                      (369, 128), (512, 256), (4, 300)])
+                                      (369, 128), (512, 256), (4, 300),
+                                      # dividends past the 512 limbs held in registers: configs[4]'s
+                                      # add outputs (737 limbs) and multiplier-sized ones
+                                      (737, 256), (3000, 700),
+                                      # divisor near / far above every dividend's degree (the
+                                      # remainder is the dividend; no table is built)
+                                      (20, 1279), (4, 5000)])
 def test_poly_rem(H, oracle, cap, sdeg):
     rng = np.random.default_rng(cap + sdeg)
     A = _rand_polys(rng, 64, cap)
@@ -263,21 +269,25 @@ def test_add_skewed_bounds(H, oracle, chain, skew):
     assert np.array_equal(dec, rdec)
 
 
-def test_add_pipeline_same_bits(H):
-    """hm_ctx_set_add_pipeline: a 2048-value add as two stream-pipelined halves writes the same
-    ciphertexts as the one-pass add (the halves use disjoint workspace and outputs)."""
+@pytest.mark.parametrize("n", [2048, 2051])
+def test_add_pipeline_same_bits(H, n):
+    """hm_ctx_set_add_pipeline: an add as two stream-pipelined halves writes the same ciphertexts
+    as the one-pass add (the halves use disjoint workspace and outputs), also for a batch whose
+    halves are not multiples of the block's 4 values, and for two pipelined adds in a row (the
+    second reuses the stream and events the first created)."""
     params = (128, 128, 1, 128)
     ctx = make_ctx(H, params, 77)
-    n = 2048
     ca = ctx.encrypt(plain(n, np.uint32, 78))
     cb = ctx.encrypt(plain(n, np.uint32, 79))
     one = ctx.apply2(H.HomomorphicAddition, ca, cb)
     ctx.set_add_pipeline(True)
     two = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    three = ctx.apply2(H.HomomorphicAddition, cb, ca)
     ctx.synchronize()
     l1, d1 = one.to_host()
-    l2, d2 = two.to_host()
-    assert_batches_equal(l1, d1, l2, d2, one.bound, n, "pipelined add")
+    for c in (two, three):
+        l2, d2 = c.to_host()
+        assert_batches_equal(l1, d1, l2, d2, one.bound, n, "pipelined add")
 
 
 def test_add_chain_mfma_unsupported(H):

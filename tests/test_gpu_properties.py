@@ -16,7 +16,7 @@ properties (the oracle alone would take minutes to hours on the whole batches).
                                                       Karatsuba = schoolbook
   configs[4] mixed add + mul-low-8, d=dp=tau=256,     the whole 2^20 global batch on one GPU through
              2^20 values                              bench.py's chunk loop: every value decrypts,
-                                                      8 sampled values bit-exact vs the oracle
+                                                      64 sampled values bit-exact vs the oracle
 Every full batch is also checked polynomial by polynomial by the residue checksum
 (oracle/residue_check.c, tests/helpers.check_residues): residues mod a random X^64 + g form a
 ring homomorphism, so each output's residue must equal the reference circuit on the inputs'.
@@ -244,7 +244,7 @@ def test_mul_low20_karatsuba_vs_schoolbook(H):
 def test_mixed_config4_full_batch(H, oracle):
     """configs[4] at its full global batch, 2^20 values at d = dp = tau = 256, on one GPU through
     bench.py's own chunk loop (the N = 1 point of the strong-scaling config): every sum and
-    product decrypts, every output polynomial of all 2^20 values passes the residue check, and 8
+    product decrypts, every output polynomial of all 2^20 values passes the residue check, and 64
     sampled values are bit-exact vs the oracle."""
     import torch
 
@@ -257,19 +257,20 @@ def test_mixed_config4_full_batch(H, oracle):
     assert ok_s == w.n and ok_p == w.n, (ok_s, ok_p)
     assert helpers.check_residues(H, "add", w.sums, w.ca, w.cb, seed=44) == w.n
     assert helpers.check_residues(H, "mul", w.prods, w.ca, w.cb, k=k, seed=45) == w.n
-    idx = np.sort(np.random.default_rng(46).choice(w.n, 8, replace=False))
+    ns = 64
+    idx = np.sort(np.random.default_rng(46).choice(w.n, ns, replace=False))
     la, da = _rows(H, w.ca, idx)
     lb, db = _rows(H, w.cb, idx)
     oracle.set_threads(8)
     try:
-        rl, rd = oracle.add_batch(la, da, w.ca.bound, lb, db, w.cb.bound, 32, 8, w.sums.bound)
+        rl, rd = oracle.add_batch(la, da, w.ca.bound, lb, db, w.cb.bound, 32, ns, w.sums.bound)
         sl, sd = _rows(H, w.sums, idx)
-        assert_batches_equal(sl, sd, rl, rd, w.sums.bound, 8, "config4 add sampled")
-        lak, dak, bk = low_bits(la, da, w.ca.bound, 8, k)
-        lbk, dbk, _ = low_bits(lb, db, w.cb.bound, 8, k)
-        rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, 8, w.prods.bound)
+        assert_batches_equal(sl, sd, rl, rd, w.sums.bound, ns, "config4 add sampled")
+        lak, dak, bk = low_bits(la, da, w.ca.bound, ns, k)
+        lbk, dbk, _ = low_bits(lb, db, w.cb.bound, ns, k)
+        rl, rd = oracle.mul_batch(lak, dak, bk, lbk, dbk, bk, k, ns, w.prods.bound)
         sl, sd = _rows(H, w.prods, idx)
-        assert_batches_equal(sl, sd, rl, rd, w.prods.bound, 8, "config4 mul sampled")
+        assert_batches_equal(sl, sd, rl, rd, w.prods.bound, ns, "config4 mul sampled")
     finally:
         oracle.set_threads(1)
     del w
