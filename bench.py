@@ -334,15 +334,23 @@ def mfma_roofline(ops, seconds, kernel, note):
             "frac": achieved / FP4_MFMA_PEAK_TFLOPS, "kernel": kernel, "note": note}
 
 
-def mul_roofline(word_pairs, n, seconds, what):
-    """MFMA roofline of a multiply (all of its launches): the carry-save circuit's algorithmic
-    bit pairs (hm_mul_cost word pairs x 1024, the planner's symbolic run of common.rs:66-105 over
-    the static bounds), 2 ops per pair, over the multiply's HIP-event time, vs the dense fp4 peak."""
-    return mfma_roofline(2.0 * 1024.0 * word_pairs * n, seconds,
-                         "mul_mfma_kernel + scan / partial-product / Karatsuba launches (whole multiply)",
-                         f"{what}: {word_pairs:.4g} word pairs (32x32 bit) per value from hm_mul_cost, "
-                         "2 ops per bit pair, over the multiply's HIP-event time on the engine "
-                         "stream (every launch of the multiply, not one kernel)")
+def mul_roofline(ctx, a_bound, b_bound, k, n, seconds, what):
+    """MFMA roofline of a multiply (all of its launches): the carry products' bit pairs as the
+    context's plan issues them (hm_mul_plan_work: schoolbook products at their static bounds,
+    Karatsuba products by their leaves; word pairs x 1024), 2 ops per pair, over the multiply's
+    HIP-event time, vs the dense fp4 peak.  The schoolbook count of the same circuit
+    (hm_mul_cost, the reference's own algorithm) rides beside it."""
+    issued = ctx.mul_plan_work(a_bound, b_bound, k)
+    school = H.mul_cost(a_bound, b_bound, k)["word_pairs"]
+    r = mfma_roofline(2.0 * 1024.0 * issued * n, seconds,
+                      "mul_mfma_kernel + scan / partial-product / Karatsuba launches (whole multiply)",
+                      f"{what}: {issued:.4g} issued carry-product word pairs (32x32 bit) per value "
+                      "(hm_mul_plan_work), 2 ops per bit pair, over the multiply's HIP-event time on "
+                      "the engine stream (every launch of the multiply, not one kernel; the partial "
+                      "products, scans and Karatsuba sums are not counted as work)")
+    r["schoolbook_word_pairs"] = school
+    r["schoolbook_equivalent_tflops"] = 2.0 * 1024.0 * school * n / seconds / 1e12
+    return r
 
 
 def s0_zero_context(device, params=PARAMS):
@@ -621,12 +629,12 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     ol8, od8 = oracle.mul_batch(o8a, o8ad, b8b, o8b, o8bd, b8b, 8, 2, co.bound)
     cpu_m8 = oracle_leg(lambda: oracle.mul_batch(o8a, o8ad, b8b, o8b, o8bd, b8b, 8, 2, co.bound), 2,
                         leg_s, "u8 homomorphic multiplies (2 per call; common.rs:66-105)")
-    w8 = H.mul_cost(ca.bound, cbb.bound, 8)["word_pairs"]
     out["u8_mul"] = {"value": n8 * mreps / wall, "unit": "u8 muls/s", "batch": n8,
                      "verified": bool(np.array_equal(got, (a8.astype(int) * b8).astype(np.uint8))),
                      "key_seed": mseed, "kernel_ms_per_batch": 1e3 * ev_s / mreps,
                      "reference_bench": "benches/u8.rs:21-29 (mul at d=dp=tau=128, delta=1)",
-                     "roofline": mul_roofline(w8, n8, ev_s / mreps, "u8 multiply"),
+                     "roofline": mul_roofline(mctx, ca.bound, cbb.bound, 8, n8, ev_s / mreps,
+                                              "u8 multiply"),
                      "cpu_baseline": cpu_m8}
     # benches/u8.rs:31-37 "decipher after mul": decrypting the 1024 u8 products (the rem-heavy
     # case of the multiply's wide outputs), one HIP graph replay per step
@@ -709,7 +717,8 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
             "bit_exact": "tests/test_golden.py (K=16 oracle fixture, 8 values), "
                          "test_gpu_properties.py (residue check of all 1024 K=16 products; "
                          "K=20 Karatsuba = schoolbook + residue check), test_gpu_parity.py",
-            "roofline": mul_roofline(cost["word_pairs"], nk, ev_s / reps, f"u32 multiply, low {k} bits"),
+            "roofline": mul_roofline(mctx, c32a.bound, c32b.bound, k, nk, ev_s / reps,
+                                     f"u32 multiply, low {k} bits"),
             "cpu_baseline": cpu_mul_low(k)}
         del cp
     full = H.mul_cost(c32a.bound, c32b.bound)
@@ -739,7 +748,7 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     w.ctx.synchronize()
     ok_s, ok_p, wall = w.verify(device, wall)
     add_pairs = chain_bit_pairs(w.ca.bound, w.cb.bound)
-    mul_wp = H.mul_cost(w.ca.bound, w.cb.bound, MUL_LOW_K)["word_pairs"]
+    mul_wp = w.ctx.mul_plan_work(w.ca.bound, w.cb.bound, MUL_LOW_K)
     out["mixed_config4"] = {
         "value": w.glob * msteps / wall,
         "unit": f"u32 values/s (one add + one mul, low {MUL_LOW_K} result bits, per value)",
@@ -752,8 +761,9 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
             2.0 * (add_pairs + 1024.0 * mul_wp) * w.glob, ev_s / msteps,
             "add_chain_mfma_kernel<25> + the multiply's launches (whole step)",
             f"per value: the add chain's {add_pairs:.4g} carry-product bit pairs (static bounds, "
-            f"DESIGN.md s4.1) + the low-{MUL_LOW_K} multiply's {mul_wp:.4g} word pairs x 1024 "
-            "(hm_mul_cost), 2 ops per bit pair, over the step's HIP-event time"),
+            f"DESIGN.md s4.1) + the low-{MUL_LOW_K} multiply's {mul_wp:.4g} issued carry-product "
+            "word pairs x 1024 (hm_mul_plan_work), 2 ops per bit pair, over the step's HIP-event "
+            "time"),
         "cpu_baseline": mixed_cpu_leg(leg_s)}
     del w
     torch.cuda.empty_cache()
@@ -1035,7 +1045,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--add-chain", choices=["auto", "mfma", "valu", "mfma_fused"], default="auto",
+    ap.add_argument("--add-chain", choices=["auto", "mfma", "valu"], default="auto",
                     help="hm_ctx_set_add_options (auto = the MFMA chain where it applies)")
     ap.add_argument("--add-pipeline", type=int, default=0,
                     help="1: big adds run as two pipelined halves; 0: one pass (engine default)")

@@ -7,7 +7,7 @@
 //                            (the matrix-core chain is adder_mfma.hip)
 #include <hip/hip_runtime.h>
 
-#include "add_prep.h"
+#include "dev_common.h"
 
 namespace hm {
 
@@ -21,6 +21,59 @@ namespace hm {
 // add_chain_kernel runs the sequential chain with ONE product per bit, P_i * carry, where P_i is
 // wave-uniform (scalar loads, scalar branches over its bits, Horner over bit positions) and the
 // carry stays in LDS for the whole chain.
+
+__device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
+    uint32_t o = 0;
+    for (uint32_t j = 0; j < i; ++j) o += cap_of(B.b[j]);
+    return o;
+}
+
+// Stage bits [i0, i0+nb) of one value's input (u64 limbs, exact degrees) into LDS words: bit
+// i0+t at dst + t*cnt, its word count at nw[t] (0 = null).  Lanes stride over the range's
+// contiguous limbs (all its bits at once, coalesced); every limb is validated against its bit's
+// degree word as in load_bit.  src/deg point at the value's first limb / degree word.
+__device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
+                           const Bounds &B, uint32_t i0, uint32_t nb, uint32_t *dst, uint32_t cnt,
+                           uint32_t *nw, int *status) {
+    const int lane = lane_id();
+    src += limb_off(B, i0);
+    deg += i0;
+    uint32_t total = 0;
+    for (uint32_t t = 0; t < nb; ++t) total += cap_of(B.b[i0 + t]);
+    uint32_t t = 0, lo = 0, hi = nb ? cap_of(B.b[i0]) : 0;
+    bool bad = false;
+    for (uint32_t g = lane; g < total; g += kWave) {
+        while (g >= hi) ++t, lo = hi, hi += cap_of(B.b[i0 + t]);
+        const uint32_t d = deg[t], k = g - lo;
+        uint64_t v = src[g];
+        if (d > B.b[i0 + t]) {
+            bad = true;
+            continue;
+        }
+        const uint32_t nl = d / 64 + 1;
+        if (k >= nl) {
+            bad |= v != 0; // limbs above the degree must be zero (layout invariant)
+            continue;
+        }
+        if (k == nl - 1) {
+            const uint32_t tb = d % 64;
+            const uint64_t keep = (~0ull) >> (63 - tb);
+            bad |= (v & ~keep) != 0;
+            v &= keep;
+            if (d > 0 && !((v >> tb) & 1ull)) bad = true;
+        }
+        dst[t * cnt + 2 * k] = (uint32_t)v;
+        dst[t * cnt + 2 * k + 1] = (uint32_t)(v >> 32);
+    }
+    if (__any(bad) && lane == 0) flag(status, HM_ERR_BAD_INPUT);
+    wsync();
+    for (uint32_t k = lane; k < nb; k += kWave) {
+        const uint32_t d = deg[k];
+        uint32_t n = d / 32 + 1;
+        if (d > B.b[i0 + k] || (d == 0 && !(dst[k * cnt] & 1u))) n = 0;
+        nw[k] = n;
+    }
+}
 
 __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
@@ -254,7 +307,7 @@ AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n) {
 
 int launch_add(const AddArgs &a, void *stream, void *ev0, void *ev1) {
     if (a.n == 0) return 0;
-    if (!a.fgrp && launch_add_prep(a, stream)) return -1; // (a fused chain computes its own)
+    if (launch_add_prep(a, stream)) return -1;
     if (ev0 && hipEventRecord((hipEvent_t)ev0, (hipStream_t)stream) != hipSuccess) return -1;
     int rc = 0;
     if (a.mfma) rc = launch_add_chain_mfma(a, stream);

@@ -26,7 +26,8 @@
 //   C     the carry as bits (u32 words), zero halo below, updated in place tile by tile from the
 //         top (tile T's output words are no longer read by tiles < T);
 //   ring  nibble images of the carry words the next tiles read (fp4 1.0 per set bit, 16 B per
-//         word, 128 slots mapped twice): a B fragment is one ds_read_b128;
+//         word, 128 slots, the first kMirror of them mirrored past the end): a B fragment is one
+//         ds_read_b128;
 //   RS    the nibble image of P_i bit-reversed: an A fragment is a 128-bit window of it.
 // A 1 KB table per block maps a byte to its 8 nibbles.
 //
@@ -34,7 +35,6 @@
 // bit 0 of its f32 encoding is the coefficient.  One v_alignbit per accumulator gathers them.
 #include <hip/hip_runtime.h>
 
-#include "add_prep.h"
 #include "mfma_gf2.h"
 
 namespace hm {
@@ -91,10 +91,20 @@ __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[NC], const uint4 *rb, 
     return acc;
 }
 
+// Ring slot of carry word w: its nibble image at slot w % kMfmaRingSlots, and slots below
+// kMirror once more past the end, so a tile's window [slot, slot + 2*NC - 1) is contiguous
+// wherever it starts: its B reads share one address and differ by immediates.
+template <int kMirror>
+__device__ __forceinline__ void ring_put(uint32_t *ring, int w, int h, uint2 nb) {
+    const int s = w & (kMfmaRingSlots - 1);
+    uint32_t *slot = &ring[s * 4 + 2 * h];
+    *(uint2 *)slot = nb;
+    if (s < kMirror) *(uint2 *)(slot + 4 * kMfmaRingSlots) = nb;
+}
+
 // Nibble images of carry words [base, base + count) into the ring (count <= 64).  Lane l writes
-// bytes 2h, 2h+1 of word base + k (k = l%32 + 32*pass, h = l/32) as two table lookups.  Every
-// slot is written twice, at s and s + kMfmaRingSlots, so a tile's window [slot, slot + 2*NC) is
-// contiguous wherever it starts: its B reads share one address and differ by immediates.
+// bytes 2h, 2h+1 of word base + k (k = l%32 + 32*pass, h = l/32) as two table lookups.
+template <int kMirror>
 __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, const uint32_t *tab,
                                           int base, int count, int lane) {
     const int h = lane >> 5;
@@ -104,9 +114,7 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
         uint2 nb;
         nb.x = tab[v & 0xFFu];
         nb.y = tab[(v >> 8) & 0xFFu];
-        uint32_t *slot = &ring[(w & (kMfmaRingSlots - 1)) * 4 + 2 * h];
-        *(uint2 *)slot = nb;
-        *(uint2 *)(slot + 4 * kMfmaRingSlots) = nb;
+        ring_put<kMirror>(ring, w, h, nb);
     }
 }
 
@@ -119,21 +127,14 @@ static_assert(kMfmaWpb <= kAddWavesPerBlock, "host LDS plan");
 
 // NC = 13: 4 waves per SIMD (configs[1]'s 4096 waves fill the chip at that), 128 VGPRs;
 // NC = 25: 2 waves per SIMD, 256 VGPRs (the 25 A fragments alone are 100)
-//
-// FUSED: the wave also computes its own records (x_i, P_i, ab_i, degrees; add_prep.h
-// prep_records), A.fgrp bits at a time into LDS (A.fgrp records after RS), instead of reading the
-// workspace add_prep_kernel wrote: no prep launch before the chain, no workspace round trip
-// through HBM.  The bits' products are VALU work in a phase of their own, between two bits' tile
-// loops, where the tile loop's registers are dead; the other waves of the SIMD keep its matrix
-// core busy meanwhile.
-template <int NC, bool FUSED>
+template <int NC>
 __global__ void __launch_bounds__(64 * kMfmaWpb)
 __attribute__((amdgpu_waves_per_eu(MfmaCfg<NC>::kWavesPerEU, MfmaCfg<NC>::kWavesPerEU)))
 add_chain_mfma_kernel(AddArgs A) {
     using Cfg = MfmaCfg<NC>;
     constexpr int kRevWords = Cfg::kRevWords, kRsWords = Cfg::kRsWords, kRec = Cfg::kRecWords;
     extern __shared__ uint32_t lds[];
-    __shared__ uint32_t stage[FUSED ? 1 : kMfmaWpb][2][FUSED ? 1 : kRec];
+    __shared__ uint32_t stage[kMfmaWpb][2][kRec];
     uint32_t *tab = lds; // byte -> 8 nibbles, fp4 1.0 (0b0010) per set bit
     for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
         uint32_t v = 0u;
@@ -147,13 +148,12 @@ add_chain_mfma_kernel(AddArgs A) {
     if (e >= A.n) return; // whole wave exits together
     const int lane = lane_id();
     const uint32_t L = A.nbits;
-    // LDS per wave: [halo][C: mf_cw][ring: 2 x 4*slots][RS: kRsWords][FUSED: fgrp records]
+    // LDS per wave: [halo][C: mf_cw][ring: kRingWords][RS: kRsWords]
     uint32_t *Ls = lds + 256 + (size_t)wave * A.chain_lds;
     uint32_t *C = Ls + Cfg::kHalo;
     uint32_t *ring = C + A.mf_cw;
-    uint32_t *RS = ring + 8 * kMfmaRingSlots;
-    uint32_t *recs = RS + kRsWords;
-    const uint32_t *ws = FUSED ? nullptr : A.ws + e * A.ws_stride;
+    uint32_t *RS = ring + Cfg::kRingWords;
+    const uint32_t *ws = A.ws + e * A.ws_stride;
     uint64_t *po = A.out.limbs + e * A.out.stride;
     uint32_t *dout = A.out.degree + e * L;
     // Bit i's workspace record, copied into stage[wave][i&1] by one LDS-DMA a bit ahead (its
@@ -179,7 +179,6 @@ add_chain_mfma_kernel(AddArgs A) {
     const uint64_t wsu = ((uint64_t)rfl((uint32_t)((uintptr_t)ws >> 32)) << 32) |
                          rfl((uint32_t)(uintptr_t)ws); // wave-uniform: SGPR base of the DMA
     auto stage_rec = [&](uint32_t i) {
-        if constexpr (FUSED) return;
         const uint32_t voff = 4u * (lbase + i * lstep);
         const uint32_t m0 = (uint32_t)(uintptr_t)&stage[wave][i & 1][0]; // LDS byte offset
         asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
@@ -206,25 +205,10 @@ add_chain_mfma_kernel(AddArgs A) {
     int degc = -1; // the carry's degree
     int tw = -1;   // > 0: the previous bit's tiles stored sum words [cntX, min(tw, cap words))
     uint32_t offo = 0;
-    const uint32_t recw = A.recw;
-    uint32_t gbase = 0; // FUSED: the bit of recs[0]
     for (uint32_t i = 0; i < L; ++i) {
         HM_PT(tw0);
-        const uint32_t *rec;
-        if constexpr (FUSED) {
-            if (i == 0 || i - gbase == A.fgrp) { // the next group's records (RS is free here)
-                gbase = i;
-                wsync();
-                prep_records(A, e, i, min(A.fgrp, L - i), recs, recw, RS);
-                // the scratch overwrote RS's zero tail (nibble words past P's image)
-                for (int k = 4 * kRevWords + lane; k < kRsWords; k += kWave) RS[k] = 0u;
-                wsync();
-            }
-            rec = recs + (i - gbase) * recw;
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
-            rec = &stage[wave][i & 1][0];
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
+        const uint32_t *rec = &stage[wave][i & 1][0];
         // s_i = x_i ^ carry_i (common.rs:43-47)
         HM_PT(t0);
         HM_PACC(3, tw0, t0);
@@ -309,7 +293,7 @@ add_chain_mfma_kernel(AddArgs A) {
         const int capn = 2 * (int)cap_of(A.ob.b[i + 1]);
         const int wlo = 32;
         // the top tile's whole window: words 32(tiles-1) - D .. + 32 + 2 NC
-        ring_fill(C, ring, tab, 32 * (tiles - 1) - D, 32 + 2 * NC, lane);
+        ring_fill<Cfg::kMirror>(C, ring, tab, 32 * (tiles - 1) - D, 32 + 2 * NC, lane);
         int ldeg = -1;
         // The accumulators start at 2^23 once per bit and keep accumulating tile after tile
         // (2^23 + every count stays below 2^24, exact): a tile's parities are bit 0 of its
@@ -349,25 +333,14 @@ add_chain_mfma_kernel(AddArgs A) {
                     fn.x = tab[fv & 0xFFu], fn.y = tab[(fv >> 8) & 0xFFu];
                 } else {
                     asm volatile("" : "+v"(fn.x), "+v"(fn.y));
-                    uint32_t *slot = &ring[(fw & (kMfmaRingSlots - 1)) * 4 + 2 * h];
-                    *(uint2 *)slot = fn;
-                    *(uint2 *)(slot + 4 * kMfmaRingSlots) = fn;
+                    ring_put<Cfg::kMirror>(ring, fw, h, fn);
                 }
             });
             __builtin_amdgcn_s_setprio(0);
-            // rows (j&3) + 8(j>>2) + 4h of column col: gather bit 0 of each accumulator, four
-            // independent 4-deep chains (nibble q = accumulators 4q .. 4q+3)
-            uint32_t nq[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t x = 0u;
-#pragma unroll
-                for (int j = 4 * q; j < 4 * q + 4; ++j) x = funnel(__float_as_uint(acc[j]), x, 1);
-                nq[q] = x >> 28; // bit j-4q = accumulator j
-            }
-            // nibble q to bits 8q .. 8q+3 (rows 8q + 4h + i sit at bit 8q + 4h + i), XOR the bits
-            // of the accumulators before this tile
-            const uint32_t tnow = nq[0] | (nq[1] << 8) | (nq[2] << 16) | (nq[3] << 24);
+            // rows (j&3) + 8(j>>2) + 4h of column col: bit 0 of each accumulator, nibble q
+            // (accumulators 4q .. 4q+3) at bits 8q .. 8q+3 (rows 8q + 4h + i sit at bit 8q + 4h + i);
+            // XOR the bits of the accumulators before this tile
+            const uint32_t tnow = acc_parities(acc);
             const uint32_t t = (tnow ^ gprev) << (4 * h);
             gprev = tnow;
             // the two lane halves' bits meet by one v_permlane32_swap (VALU; no LDS round trip)
@@ -398,18 +371,12 @@ int launch_add_chain_mfma(const AddArgs &a, void *stream) {
     const int wpb = kMfmaWpb;
     const uint64_t blocks = (a.n + wpb - 1) / wpb;
     const size_t lds = (256 + (size_t)a.chain_lds * wpb) * 4;
-#define HM_LAUNCH_CHAIN(NCV, F)                                                                   \
-    hipLaunchKernelGGL((add_chain_mfma_kernel<NCV, F>), dim3((unsigned)blocks), dim3(64 * wpb), \
-                       lds, (hipStream_t)stream, a)
-    if (a.mfma == MfmaCfg<13>::kChunks) {
-        if (a.fgrp) HM_LAUNCH_CHAIN(13, true);
-        else HM_LAUNCH_CHAIN(13, false);
-    } else if (a.mfma == MfmaCfg<25>::kChunks) {
-        if (a.fgrp) HM_LAUNCH_CHAIN(25, true);
-        else HM_LAUNCH_CHAIN(25, false);
-    } else {
-        return -1;
-    }
+#define HM_LAUNCH_CHAIN(NCV)                                                                      \
+    hipLaunchKernelGGL((add_chain_mfma_kernel<NCV>), dim3((unsigned)blocks), dim3(64 * wpb), lds,  \
+                       (hipStream_t)stream, a)
+    if (a.mfma == MfmaCfg<13>::kChunks) HM_LAUNCH_CHAIN(13);
+    else if (a.mfma == MfmaCfg<25>::kChunks) HM_LAUNCH_CHAIN(25);
+    else return -1;
 #undef HM_LAUNCH_CHAIN
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

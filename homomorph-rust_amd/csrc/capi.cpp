@@ -459,7 +459,7 @@ hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) 
 }
 
 hm_status hm_ctx_set_add_options(hm_ctx *c, uint32_t chain) {
-    if (!c || chain > HM_ADD_CHAIN_MFMA_FUSED) return HM_ERR_INVALID_ARGUMENT;
+    if (!c || chain > HM_ADD_CHAIN_VALU) return HM_ERR_INVALID_ARGUMENT;
     c->add_chain = chain;
     return HM_OK;
 }
@@ -549,6 +549,13 @@ hm_status hm_mul_cost(uint32_t L, uint32_t k, const uint32_t *a, const uint32_t 
     if (out_bytes) *out_bytes = o;
     if (max_degree) *max_degree = m;
     return HM_OK;
+}
+
+hm_status hm_mul_plan_work(hm_ctx *c, uint32_t L, uint32_t k, const uint32_t *a, const uint32_t *b,
+                          int is_signed, double *word_pairs) {
+    if (!c || !a || !b || !word_pairs || L == 0 || L > HM_MAX_BITS || k == 0 || k > L)
+        return HM_ERR_INVALID_ARGUMENT;
+    return mul_plan_work(c, L, k, a, b, is_signed != 0 && k == L, *word_pairs);
 }
 
 hm_status hm_gate_out_bounds(hm_op g, uint32_t L, const uint32_t *a, const uint32_t *b,
@@ -727,45 +734,26 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         // for one block
         auto plan = [&](auto cfg) -> uint32_t {
             using Cfg = decltype(cfg);
-            const uint32_t lds = Cfg::kHalo + mf_cw + 8 * kMfmaRingSlots + Cfg::kRsWords;
+            const uint32_t lds = Cfg::kHalo + mf_cw + Cfg::kRingWords + Cfg::kRsWords;
             const bool fits = maxPw <= 2 * Cfg::kChunks - 1 && cntAB <= 64 && cntX <= 32 &&
                               cntX + cntP + cntAB + 2 <= (uint32_t)Cfg::kRecWords &&
                               (256 + (size_t)lds * kAddWavesPerBlock + Cfg::kStageWords) * 4 <=
                                   160 * 1024;
             return fits ? lds : 0u;
         };
-        uint32_t nc = 0, lds = 0, rs = 0, wpe = 0;
-        if ((lds = plan(MfmaCfg<13>{}))) nc = 13, rs = MfmaCfg<13>::kRsWords, wpe = MfmaCfg<13>::kWavesPerEU;
-        else if ((lds = plan(MfmaCfg<25>{}))) nc = 25, rs = MfmaCfg<25>::kRsWords, wpe = MfmaCfg<25>::kWavesPerEU;
+        uint32_t nc = 0, lds = 0;
+        if ((lds = plan(MfmaCfg<13>{}))) nc = 13;
+        else if ((lds = plan(MfmaCfg<25>{}))) nc = 25;
         if (!c->fp4_mfma) nc = 0;
         A.mfma = c->add_chain != HM_ADD_CHAIN_VALU ? nc : 0u;
-        if ((c->add_chain == HM_ADD_CHAIN_MFMA || c->add_chain == HM_ADD_CHAIN_MFMA_FUSED) && !nc)
-            return HM_ERR_UNSUPPORTED;
+        if (c->add_chain == HM_ADD_CHAIN_MFMA && !nc) return HM_ERR_UNSUPPORTED;
         if (A.mfma) A.mf_cw = mf_cw, A.chain_lds = lds;
-        // Fused prep (adder_mfma.hip FUSED): the chain's wave computes its records fgrp bits at a
-        // time into LDS after RS.  The largest group whose rows fit one pass of 64 lanes, whose
-        // staged inputs fit the RS scratch, and whose records leave the chain its full occupancy
-        // (kWavesPerEU blocks of 4 waves per CU); none fits -> the separate prep launch.
-        if (A.mfma && c->add_chain == HM_ADD_CHAIN_MFMA_FUSED && !c->add_pipe) {
-            const uint32_t recw = even(cntX + cntP + cntAB + 2);
-            for (uint32_t g = std::min<uint32_t>(L, std::max<uint32_t>(1, 64 / cntX)); g >= 1; --g) {
-                const uint32_t wl = lds + g * recw;
-                const size_t block = (256 + (size_t)wl * kAddWavesPerBlock) * 4 + 8;
-                if (g * (cntA + cntB + 2) <= rs && block <= (size_t)160 * 1024 / wpe) {
-                    A.fgrp = g, A.recw = recw, A.chain_lds = wl;
-                    break;
-                }
-            }
-            if (!A.fgrp) return HM_ERR_UNSUPPORTED;
-        }
     }
+    A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
+    const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
     DeviceGuard g(c->device);
-    if (!A.fgrp) { // the prep launch's workspace (the fused chain keeps its records in LDS)
-        A.ws_stride = ((uint64_t)L * (cntAB + cntP + 2 + cntX) + 63) & ~(uint64_t)63;
-        const size_t bytes = (size_t)A.ws_stride * 4 * a->n;
-        HM_HIP(c, grow(c, c->d_ws_add, c->ws_add_bytes, bytes));
-        A.ws = c->d_ws_add;
-    }
+    HM_HIP(c, grow(c, c->d_ws_add, c->ws_add_bytes, bytes));
+    A.ws = c->d_ws_add;
     A.a = batch_arg(a), A.b = batch_arg(b), A.out = batch_arg(out);
     A.n = a->n, A.nbits = L;
     A.status = c->d_status;

@@ -170,6 +170,10 @@ inline hm_status check_batch(const hm_batch *b, bool need_limbs = true) {
 hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t K, bool is_signed,
                       hm_batch *out);
 void mul_plans_release(hm_ctx *c);
+// The word pairs of the carry products as the context's plan runs them (Karatsuba products by
+// their leaves), for the low K output bits of the nbits-bit circuit (hm_mul_plan_work).
+hm_status mul_plan_work(hm_ctx *c, uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,
+                        bool is_signed, double &executed);
 // Degree bounds of the K low output bits of the nbits-bit circuit (-1 = always null); false when a
 // bound exceeds the engine's 2^30 limit.  The same symbolic walk as the plan.
 bool mul_result_bounds(uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,

@@ -243,11 +243,7 @@ __device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__rest
             lo = holey_fold(zl), hi = holey_fold(zh);
         }
         const uint32_t w = lo ^ hiprev;
-#if defined(HM_FUSE_DIAG) && HM_FUSE_DIAG == 3
-        if (w) out[k] = w; // diagnostic: plain stores instead of LDS atomics (wrong results)
-#else
         if (w) atomicXor(&out[k], w);
-#endif
         hiprev = hi;
     }
 }

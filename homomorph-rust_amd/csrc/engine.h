@@ -43,9 +43,6 @@ struct AddArgs {
     uint32_t mfma;                    // chain on the matrix cores (adder_mfma.hip): its chunk count
                                       // NC (MfmaCfg), 0 = the VALU chain
     uint32_t mf_cw;                   // MFMA chain: carry bit words (tiles, window overhang)
-    uint32_t fgrp;                    // MFMA chain: > 0 = fused (no prep launch): bits per group
-                                      // whose records the chain's wave computes itself
-    uint32_t recw;                    // fused: words per LDS record (x, P, ab, two degrees)
     int *status;
     Bounds ab, bb, ob;
 };
@@ -291,6 +288,11 @@ template <int NC> struct MfmaCfg {
     static constexpr int kRecWords = NC <= 16 ? 64 : 128;
     static constexpr int kWavesPerEU = NC <= 16 ? 4 : 2;
     static constexpr int kStageWords = 2 * kRecWords * kAddWavesPerBlock; // static LDS per block
+    // ring slots mirrored past the end (slot s < kMirror also at kMfmaRingSlots + s), so every
+    // lane's window of 2 NC - 1 slots is contiguous wherever it starts
+    static constexpr int kMirror = NC <= 16 ? 32 : 64;
+    static constexpr int kRingWords = 4 * (kMfmaRingSlots + kMirror);
+    static_assert(2 * NC - 1 <= kMirror, "ring mirror");
     static_assert(32 + 2 * NC + 32 <= kMfmaRingSlots, "ring window");
 };
 constexpr size_t kEncTableBytes = 96 * 1024; // largest encryption nibble table staged in LDS

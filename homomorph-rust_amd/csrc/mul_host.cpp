@@ -98,6 +98,7 @@ struct MulPlan {
     size_t off_mspans = 0, off_ppm = 0;
     size_t off_ka_sums = 0, off_ka_vtasks = 0, off_ka_vtiles = 0, off_ka_combs = 0;
     uint64_t work = 0; // word-pair products (statistics)
+    std::vector<double> prod_pairs; // per carry product (P.prod): its schoolbook word pairs
 };
 
 namespace {
@@ -263,6 +264,7 @@ bool build_plan(MulPlan &P) {
                 if (wp <= wx) P.prod.push_back({pslot, x.slot, cs});
                 else P.prod.push_back({x.slot, pslot, cs});
                 P.work += (uint64_t)(pb / 32 + 1) * (uint64_t)(x.bound / 32 + 1);
+                P.prod_pairs.push_back((double)(pb / 32 + 1) * (double)(x.bound / 32 + 1));
                 cur.push_back({cs, cbnd});
             }
             pb = std::max(pb, x.bound); // result ^= x_t
@@ -493,6 +495,26 @@ void mul_cost_model(uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_
         out_bytes += 8 * (std::floor(std::max(pb, 0.0) / 64) + 1);
         prev.swap(cur);
     }
+}
+
+hm_status mul_plan_work(hm_ctx *c, uint32_t nbits, uint32_t K, const uint32_t *a, const uint32_t *b,
+                        bool is_signed, double &executed) {
+    MulPlan *P = nullptr;
+    if (hm_status st = get_plan(c, nbits, K, a, b, is_signed, P); st) return st;
+    // carries as the plan runs them: a schoolbook product's word pairs at its static bounds (as
+    // hm_mul_cost counts them), a Karatsuba product's leaf products instead (a product's output
+    // slot is its own, so it identifies the product)
+    executed = 0;
+    std::vector<bool> ka(P->slots.size(), false);
+    for (const auto &col : P->cols)
+        for (const KaProg &pg : col.ka) {
+            ka[pg.out] = true;
+            for (uint32_t t = pg.vtask; t < pg.vtask + pg.nvtask; ++t)
+                executed += (double)P->ka_vtasks[t].nu * (double)P->ka_vtasks[t].nv;
+        }
+    for (size_t k = 0; k < P->prod.size(); ++k)
+        if (!ka[P->prod[k].out]) executed += P->prod_pairs[k];
+    return HM_OK;
 }
 
 void mul_plans_release(hm_ctx *c) {

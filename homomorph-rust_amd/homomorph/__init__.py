@@ -428,7 +428,7 @@ class Context:
                               "(run more warm-up calls)")
         return EngineGraph(self, g, gen)
 
-    ADD_CHAINS = {"auto": 0, "mfma": 1, "valu": 2, "mfma_fused": 3}
+    ADD_CHAINS = {"auto": 0, "mfma": 1, "valu": 2}
 
     def set_add_options(self, chain: str = "auto"):
         """hm_ctx_set_add_options: where the adder's carry products run -- "mfma" (fp4 matrix
@@ -646,6 +646,16 @@ class Context:
                                              ctypes.byref(cb), ctypes.byref(co))
         self._launch(fn, op.__name__)
         return out
+
+    def mul_plan_work(self, a_bound, b_bound, k=None, signed=False) -> float:
+        """hm_mul_plan_work: the carry products' word pairs as this context's plan runs them
+        (Karatsuba products by their leaves) for the low k output bits (all when k is None)."""
+        a, b = _u32(a_bound), _u32(b_bound)
+        k = a.size if k is None else int(k)
+        w = ctypes.c_double()
+        _check(lib().hm_mul_plan_work(self._h, a.size, k, _p32(a), _p32(b), int(signed),
+                                      ctypes.byref(w)), "hm_mul_plan_work")
+        return w.value
 
     def mul_low(self, a: Ciphered, b: Ciphered, k: int) -> Ciphered:
         """Low k bits of HomomorphicMultiplication on a and b: bit-exact

@@ -82,6 +82,8 @@ SIGNATURES = {
     "hm_mul_cost": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double)]),
+    "hm_mul_plan_work": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double)]),
     "hm_gate_out_bounds": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, u32p, u32p, u32p]),
     "hm_batch_stride": (ctypes.c_uint64, [ctypes.c_uint32, u32p]),
     "hm_encrypt_batch": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.POINTER(HmBatch)]),

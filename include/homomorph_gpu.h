@@ -178,11 +178,6 @@ hm_status hm_ctx_set_mul_products(hm_ctx *ctx, uint32_t products);
 #define HM_ADD_CHAIN_AUTO 0u
 #define HM_ADD_CHAIN_MFMA 1u
 #define HM_ADD_CHAIN_VALU 2u
-/* The MFMA chain computing its carry-independent products (ab_i, P_i) in the chain kernel's own
- * waves, a group of bits at a time into LDS, instead of a separate prep launch writing an HBM
- * workspace (AUTO and MFMA).  Same results; HM_ERR_UNSUPPORTED where the records do not fit the
- * chain's LDS at full occupancy. */
-#define HM_ADD_CHAIN_MFMA_FUSED 3u
 hm_status hm_ctx_set_add_options(hm_ctx *ctx, uint32_t chain);
 
 /* Adder pipelining (no effect on results; off by default: measured no faster on configs[1],
@@ -226,6 +221,14 @@ hm_status hm_mul_out_bounds(uint32_t nbits, const uint32_t *a_bound, const uint3
  * NULL. */
 hm_status hm_mul_cost(uint32_t nbits, uint32_t k, const uint32_t *a_bound, const uint32_t *b_bound,
                       int is_signed, double *word_pairs, double *out_bytes, double *max_degree);
+/* The same carry products as the context's plan for hm_mul_low_batch / hm_mul_batch (k = nbits)
+ * runs them, with the context's strategy options (hm_ctx_set_mul_options, _products): a schoolbook
+ * product counts its word pairs at the static bounds (as hm_mul_cost does), a Karatsuba product its
+ * leaf products' word pairs.  No device work runs; the plan is built and cached (its task tables
+ * uploaded) as the multiply would; HM_ERR_UNSUPPORTED beyond the engine's limits.  The bench's
+ * multiply rooflines use it as the issued work. */
+hm_status hm_mul_plan_work(hm_ctx *ctx, uint32_t nbits, uint32_t k, const uint32_t *a_bound,
+                           const uint32_t *b_bound, int is_signed, double *word_pairs);
 /* Output bounds of a gate (common.rs:5-35). */
 hm_status hm_gate_out_bounds(hm_op gate, uint32_t nbits, const uint32_t *a_bound,
                              const uint32_t *b_bound, uint32_t *out_bound);

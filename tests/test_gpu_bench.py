@@ -46,6 +46,7 @@ def test_bench_every_line_has_roofline_and_cpu_baseline():
         r = line["roofline"]
         assert r["bound"] in ("hbm", "mfma") and r["peak"] > 0 and r["achieved"] > 0, name
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9, name
+        assert r["frac"] <= 1.0, (name, r["frac"])  # issued work, never an algorithm's count
         c = line["cpu_baseline"]
         assert c["value"] > 0 and c["cores"] == 1 and c["kind"] == "port", name
     assert sec["u8_mul"]["verified"] and sec["u8_decrypt_after_mul"]["verified"]

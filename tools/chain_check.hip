@@ -112,9 +112,9 @@ static int run_case(int L, int npw, int abw, int mode, int pbit, int cbit, bool 
     const uint32_t tiles = (uint32_t)((maxw + 31) / 32) + 1;
     A.mf_cw = 32 * tiles + 64;
     A.mfma = npw <= 25 ? 13 : 25;
-    A.chain_lds = (A.mfma == 13 ? MfmaCfg<13>::kHalo + MfmaCfg<13>::kRsWords
-                                : MfmaCfg<25>::kHalo + MfmaCfg<25>::kRsWords) +
-                  A.mf_cw + 8 * kMfmaRingSlots;
+    A.chain_lds = (A.mfma == 13 ? MfmaCfg<13>::kHalo + MfmaCfg<13>::kRsWords + MfmaCfg<13>::kRingWords
+                                : MfmaCfg<25>::kHalo + MfmaCfg<25>::kRsWords + MfmaCfg<25>::kRingWords) +
+                  A.mf_cw;
     uint32_t *dws;
     uint64_t *dout;
     uint32_t *ddeg;
@@ -201,9 +201,9 @@ static int timing(int nvals, bool wide) {
     const uint32_t tiles = (maxw + 31) / 32;
     A.mf_cw = 32 * tiles + 64;
     A.mfma = wide ? 25 : 13;
-    A.chain_lds = (wide ? MfmaCfg<25>::kHalo + MfmaCfg<25>::kRsWords
-                        : MfmaCfg<13>::kHalo + MfmaCfg<13>::kRsWords) +
-                  A.mf_cw + 8 * kMfmaRingSlots;
+    A.chain_lds = (wide ? MfmaCfg<25>::kHalo + MfmaCfg<25>::kRsWords + MfmaCfg<25>::kRingWords
+                        : MfmaCfg<13>::kHalo + MfmaCfg<13>::kRsWords + MfmaCfg<13>::kRingWords) +
+                  A.mf_cw;
     uint32_t *dws, *ddeg;
     uint64_t *dout;
     int *dst;

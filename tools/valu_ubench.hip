@@ -46,6 +46,11 @@ __global__ void __launch_bounds__(256) k(uint32_t *out, uint32_t seed) {
             if (OP == 27) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(aa[j]) : "v"(a[j]), "v"(b) : "vcc");
             if (OP == 15) asm volatile("v_xor_b32 %0, %0, %1 row_shr:1 bound_ctrl:0" : "+v"(a[j]) : "v"(b));
             if (OP == 14) asm volatile("v_pk_mov_b32 %0, %1, %0 op_sel:[1,0]" : "+v"(aa[j]) : "v"(aa[(j + 1) % CHAINS]));
+            if (OP == 28) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+            if (OP == 29) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+            if (OP == 32) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "s"(s));
+            if (OP == 30) asm volatile("v_lshlrev_b32 %0, 1, %0\n\tv_xor_b32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+            if (OP == 31) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a[j]), "+v"(c));
         }
     }
     uint32_t r = s;
@@ -103,6 +108,11 @@ int main() {
         run<13>("lshl_b64", w);
         run<14>("pk_mov", w);
         run<15>("xor_dpp", w);
+        run<28>("perm", w);
+        run<32>("perm_vvs", w);
+        run<29>("and_or", w);
+        run<30>("lshl+xor", w);
+        run<31>("permlane32_swap", w);
     }
     return 0;
 }
