@@ -54,6 +54,20 @@ struct KaProg {
     std::vector<std::array<uint32_t, 3>> combs;  // per level k..1: (first KaComb, count, h)
 };
 
+// One launch of MFMA products (mul_mfma_kernel<false>): spans of `span` output tiles, the LDS
+// slices sized by its largest operands.  A column's schoolbook products are split by the shorter
+// operand's size into launches of their own, so the narrow products' small slices are not sized
+// for the wide products' (and their spans cover their outputs, not 16 tiles of mostly nothing).
+struct MfLaunch {
+    uint32_t spans = 0, nspans = 0; // MulTile range in mspans
+    uint32_t vmax = 0, umax = 0, span = 0;
+};
+// shorter operand (words) of the narrow class of schoolbook carries
+#ifndef HM_MF_NARROW_WORDS
+#define HM_MF_NARROW_WORDS 72
+#endif
+constexpr uint32_t kMfNarrowWords = HM_MF_NARROW_WORDS;
+
 struct MulPlan {
     // key
     uint32_t L = 0, K = 0;
@@ -67,16 +81,15 @@ struct MulPlan {
     std::vector<int64_t> res_bound;
     struct Col {
         uint32_t pp, npp;          // MulPPTask offset / count (in tasks): the VALU partial products
-        uint32_t ppm, ppm_spans, nppm_spans; // MFMA partial products: MulProdTask offset (ppm
-                                             // list), their spans (mspans offset / count)
-        uint32_t ppm_vmax, ppm_umax;
+        uint32_t ppm;              // MFMA partial products: MulProdTask offset (ppm list)
+        MfLaunch ppl;              // ... their launch
         uint32_t items, nitems;    // u32 offset of the item slot ids
         uint32_t prefix;           // u32 offset of the prefix slot ids (nitems - 1)
         uint32_t res;              // result degree slot
         uint32_t maxwords;         // widest prefix / result
         uint32_t prod;             // MulProdTask offset (in tasks)
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
-        uint32_t mspans, nmspans, mvmax, mumax;  // MFMA products: MulTile spans (offset / count), max V
+        MfLaunch mfl[2];                  // MFMA schoolbook products: narrow, wide
         std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
@@ -216,8 +229,8 @@ bool build_plan(MulPlan &P) {
         reg[creg].used = 0;
         std::vector<Item> items;
         col.pp = (uint32_t)P.pp.size();
-        col.ppm = (uint32_t)P.ppm.size(), col.ppm_vmax = 0, col.ppm_umax = 0;
-        std::vector<MulTile> ppm_spans;
+        col.ppm = (uint32_t)P.ppm.size();
+        uint32_t ppm_omax = 0;
         for (uint32_t j = 0; j <= i; ++j) {
             const int64_t bnd = (int64_t)P.ab[j] + P.bb[i - j];
             if (bnd > kBoundLimit) return false;
@@ -227,21 +240,23 @@ bool build_plan(MulPlan &P) {
             const uint32_t wa = P.slots[sa].words, wb = P.slots[sb].words;
             // on the matrix cores unless a signed corner (+1) or a narrow operand
             if (P.mfma && !flip && std::min(wa, wb) >= kMfMinWords) {
-                const uint32_t t = (uint32_t)P.ppm.size() - col.ppm;
                 P.ppm.push_back(wa <= wb ? MulProdTask{sa, sb, s} : MulProdTask{sb, sa, s});
-                for (uint32_t base = 0; base < P.slots[s].words; base += 32 * kMfSpan)
-                    ppm_spans.push_back({t, base});
-                col.ppm_vmax = std::max(col.ppm_vmax, std::max(wa, wb));
-                col.ppm_umax = std::max(col.ppm_umax, std::min(wa, wb));
+                col.ppl.vmax = std::max(col.ppl.vmax, std::max(wa, wb));
+                col.ppl.umax = std::max(col.ppl.umax, std::min(wa, wb));
+                ppm_omax = std::max(ppm_omax, P.slots[s].words);
             } else {
                 P.pp.push_back({sa, sb, s, flip ? 1u : 0u});
             }
             items.push_back({s, bnd});
         }
         col.npp = (uint32_t)P.pp.size() - col.pp;
-        col.ppm_spans = (uint32_t)P.mspans.size();
-        P.mspans.insert(P.mspans.end(), ppm_spans.begin(), ppm_spans.end());
-        col.nppm_spans = (uint32_t)ppm_spans.size();
+        // spans of the partial products: their whole (short) outputs, at most kMfSpan tiles
+        col.ppl.span = std::min<uint32_t>(kMfSpan, (ppm_omax + 31) / 32);
+        col.ppl.spans = (uint32_t)P.mspans.size();
+        for (uint32_t t = 0; t < (uint32_t)P.ppm.size() - col.ppm; ++t)
+            for (uint32_t base = 0; base < P.slots[P.ppm[col.ppm + t].out].words; base += 32 * col.ppl.span)
+                P.mspans.push_back({t, base});
+        col.ppl.nspans = (uint32_t)P.mspans.size() - col.ppl.spans;
         items.insert(items.end(), prev.begin(), prev.end());
         const bool push = i + 1 < K;
         std::vector<Item> cur;
@@ -335,15 +350,17 @@ bool build_plan(MulPlan &P) {
         // tiles of this column's schoolbook products: MFMA spans where the uniform operand has
         // at least kMfMinWords words (mfma plans), the rest grouped by per-lane VALU tile width
         std::vector<MulTile> byw[kNW];
-        col.mspans = (uint32_t)P.mspans.size(), col.mvmax = 0, col.mumax = 0;
+        std::vector<uint32_t> mfk[2]; // MFMA schoolbook products by class
+        uint32_t omax[2] = {0, 0};
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
             if (is_ka[k - col.prod]) continue;
-            if (P.mfma && P.slots[P.prod[k].u].words >= kMfMinWords) {
-                const uint32_t nout = P.slots[P.prod[k].out].words;
-                for (uint32_t base = 0; base < nout; base += 32 * kMfSpan)
-                    P.mspans.push_back({k - col.prod, base});
-                col.mvmax = std::max(col.mvmax, P.slots[P.prod[k].v].words);
-                col.mumax = std::max(col.mumax, P.slots[P.prod[k].u].words);
+            const uint32_t uw = P.slots[P.prod[k].u].words;
+            if (P.mfma && uw >= kMfMinWords) {
+                const int cl = uw <= kMfNarrowWords ? 0 : 1;
+                mfk[cl].push_back(k);
+                col.mfl[cl].vmax = std::max(col.mfl[cl].vmax, P.slots[P.prod[k].v].words);
+                col.mfl[cl].umax = std::max(col.mfl[cl].umax, uw);
+                omax[cl] = std::max(omax[cl], P.slots[P.prod[k].out].words);
                 continue;
             }
             const uint32_t nout = P.slots[P.prod[k].out].words;
@@ -357,7 +374,15 @@ bool build_plan(MulPlan &P) {
             const uint32_t span = 64 * kMulTileW[wc];
             for (uint32_t base = 0; base < nout; base += span) byw[wc].push_back({k - col.prod, base});
         }
-        col.nmspans = (uint32_t)P.mspans.size() - col.mspans;
+        for (int cl = 0; cl < 2; ++cl) {
+            MfLaunch &m = col.mfl[cl];
+            m.span = std::min<uint32_t>(kMfSpan, std::max<uint32_t>(1, (omax[cl] + 31) / 32));
+            m.spans = (uint32_t)P.mspans.size();
+            for (uint32_t k : mfk[cl])
+                for (uint32_t base = 0; base < P.slots[P.prod[k].out].words; base += 32 * m.span)
+                    P.mspans.push_back({k - col.prod, base});
+            m.nspans = (uint32_t)P.mspans.size() - m.spans;
+        }
         for (uint32_t q = 0; q < kNW; ++q) {
             col.tiles[q] = (uint32_t)P.tiles.size();
             col.ntiles[q] = (uint32_t)byw[q].size();
@@ -614,15 +639,17 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             MulPPArgs pp{};
             pp.B = B, pp.tasks = (const MulPPTask *)(T + P->off_pp) + col.pp, pp.ntasks = col.npp;
             if (launch_mul_pp(pp, c->stream)) return hip_fail(c, hipGetLastError());
-            if (col.nppm_spans) {
+            auto mf_launch = [&](const MfLaunch &m, size_t task_off, uint32_t task0) -> hm_status {
+                if (!m.nspans) return HM_OK;
                 MulMfmaArgs mf{};
-                mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_ppm) + col.ppm;
-                mf.spans = (const MulTile *)(T + P->off_mspans) + col.ppm_spans;
-                mf.nitems = col.nppm_spans, mf.span = kMfSpan;
-                mf.vmax = col.ppm_vmax, mf.umax = col.ppm_umax;
+                mf.B = B, mf.tasks = (const MulProdTask *)(T + task_off) + task0;
+                mf.spans = (const MulTile *)(T + P->off_mspans) + m.spans;
+                mf.nitems = m.nspans, mf.span = m.span;
+                mf.vmax = m.vmax, mf.umax = m.umax;
                 mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span, mf.umax);
-                if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
-            }
+                return launch_mul_mfma(mf, false, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
+            };
+            if (hm_status st = mf_launch(col.ppl, P->off_ppm, col.ppm); st) return st;
             MulScanArgs sc{};
             sc.B = B;
             sc.items = (const uint32_t *)(T + P->off_lists) + col.items;
@@ -632,15 +659,8 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             sc.out = oa, sc.out_off = ooff[i], sc.out_cap = cap_of(out->bound[i]);
             sc.chunks = (std::max(col.maxwords, 2 * sc.out_cap) + 255) / 256;
             if (launch_mul_scan(sc, c->stream)) return hip_fail(c, hipGetLastError());
-            if (col.nmspans) {
-                MulMfmaArgs mf{};
-                mf.B = B, mf.tasks = (const MulProdTask *)(T + P->off_prod) + col.prod;
-                mf.spans = (const MulTile *)(T + P->off_mspans) + col.mspans;
-                mf.nitems = col.nmspans, mf.span = kMfSpan;
-                mf.vmax = col.mvmax, mf.umax = col.mumax;
-                mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span, mf.umax);
-                if (launch_mul_mfma(mf, false, c->stream)) return hip_fail(c, hipGetLastError());
-            }
+            for (const MfLaunch &m : col.mfl)
+                if (hm_status st = mf_launch(m, P->off_prod, col.prod); st) return st;
             for (uint32_t q = 0; q < kNW; ++q) {
                 if (!col.ntiles[q]) continue;
                 MulProdArgs pr{};
