@@ -190,6 +190,25 @@ struct MulMfmaArgs {
     uint32_t vmax, wave_words;
     uint32_t umax;        // largest U (words; blocks of at most kMfUB): sizes the U image
 };
+// Partial products grouped by their shared factor a_j (mul_mfma.hip mul_ppg_kernel): every
+// a_j * b_k of the plan in one launch before the columns, one wave per (value, a_j), a_j's A
+// fragments built once for all of its products (a_j within kMfPPGWords words: one chunk group).
+constexpr uint32_t kMfPPGWords = 34;
+struct MulPPGroup {
+    uint32_t u;            // slot of a_j (the shared factor)
+    uint32_t first, count; // its products: items [first, first + count)
+};
+struct MulPPItem {
+    uint32_t v, out;       // b_k's slot, the product's slot
+};
+struct MulPPGArgs {
+    MulBase B;
+    const MulPPGroup *groups;
+    const MulPPItem *items;
+    uint32_t ngroups;                 // groups per value
+    uint32_t umax, vmax, span;        // largest factor, other factor (words), output tiles
+    uint32_t wave_words;
+};
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
 struct KaComb {
     uint32_t z0, z1, z2; // child results, 2h words each (z1 may be kKaNone)
@@ -256,6 +275,7 @@ int launch_mul_final(const MulFinalArgs &a, void *stream);
 int launch_ka_sum(const KaSumArgs &a, void *stream);
 int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
+int launch_mul_ppg(const MulPPGArgs &a, void *stream);
 uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);
 int launch_mul_deg(const MulDegArgs &a, void *stream);

@@ -101,6 +101,13 @@ struct MulPlan {
     std::vector<MulTile> tiles;
     std::vector<MulTile> mspans; // MFMA spans {task, first output word} of the schoolbook products
     std::vector<MulProdTask> ppm; // partial products a_j * b_k run on the matrix cores
+    // ... or, when every one fits (kMfPPGWords), all of them in one launch before the columns,
+    // grouped by a_j (mul_ppg_kernel)
+    bool ppg = false;
+    std::vector<MulPPGroup> ppg_groups;
+    std::vector<MulPPItem> ppg_items;
+    uint32_t ppg_umax = 0, ppg_vmax = 0, ppg_span = 0;
+    size_t off_ppg_groups = 0, off_ppg_items = 0;
     std::vector<KaSum> ka_sums;
     std::vector<MulVTask> ka_vtasks;
     std::vector<MulVTile> ka_vtiles;
@@ -202,7 +209,7 @@ struct KaBuild {
 // even columns / carries of odd columns); regions are placed once their maxima are known.
 bool build_plan(MulPlan &P) {
     const uint32_t K = P.K;
-    enum { IN, PP, PRE, CA, CB, KA, NREG };
+    enum { IN, PP, PRE, CA, CB, KA, PPA, NREG };
     Region reg[NREG];
     std::vector<uint8_t> slot_reg;
     auto new_slot = [&](int r, int64_t bound) -> uint32_t {
@@ -219,6 +226,35 @@ bool build_plan(MulPlan &P) {
         uint32_t slot;
         int64_t bound;
     };
+    // Grouped partial products: every a_j * b_k (j + k < K) on the matrix cores, all in one
+    // launch, when every factor has at most kMfPPGWords words (and at least kMfMinWords); their
+    // slots live in a region of their own (PPA), not reused column by column.  The signed
+    // corners (+1, column L-1) stay VALU tasks of their column.
+    std::vector<std::vector<uint32_t>> pp_slot(K, std::vector<uint32_t>(K, ~0u));
+    P.ppg = P.mfma;
+    for (uint32_t j = 0; j < K && P.ppg; ++j) {
+        const uint32_t wa = (uint32_t)(P.ab[j] / 32 + 1), wb = (uint32_t)(P.bb[j] / 32 + 1);
+        if (std::max(wa, wb) > kMfPPGWords || std::min(wa, wb) < kMfMinWords) P.ppg = false;
+    }
+    if (P.ppg) {
+        uint32_t omax = 0;
+        for (uint32_t j = 0; j < K; ++j) {
+            MulPPGroup g{j, (uint32_t)P.ppg_items.size(), 0};
+            for (uint32_t k = 0; j + k < K; ++k) {
+                if (pp_flip(P.is_signed, P.L, j + k, j)) continue;
+                const int64_t bnd = (int64_t)P.ab[j] + P.bb[k];
+                const uint32_t s = new_slot(PPA, bnd);
+                pp_slot[j][k] = s;
+                P.ppg_items.push_back({K + k, s});
+                omax = std::max(omax, P.slots[s].words);
+                P.ppg_vmax = std::max(P.ppg_vmax, (uint32_t)(P.bb[k] / 32 + 1));
+            }
+            g.count = (uint32_t)P.ppg_items.size() - g.first;
+            P.ppg_umax = std::max(P.ppg_umax, (uint32_t)(P.ab[j] / 32 + 1));
+            if (g.count) P.ppg_groups.push_back(g);
+        }
+        P.ppg_span = std::min<uint32_t>(kMfSpan, std::max<uint32_t>(1, (omax + 31) / 32));
+    }
     std::vector<Item> prev;
     P.res_bound.assign(K, -1);
     for (uint32_t i = 0; i < K; ++i) {
@@ -234,6 +270,10 @@ bool build_plan(MulPlan &P) {
         for (uint32_t j = 0; j <= i; ++j) {
             const int64_t bnd = (int64_t)P.ab[j] + P.bb[i - j];
             if (bnd > kBoundLimit) return false;
+            if (pp_slot[j][i - j] != ~0u) { // computed by the grouped launch
+                items.push_back({pp_slot[j][i - j], bnd});
+                continue;
+            }
             const uint32_t s = new_slot(PP, bnd);
             const bool flip = pp_flip(P.is_signed, P.L, i, j);
             const uint32_t sa = j, sb = K + (i - j);
@@ -423,6 +463,8 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
     P.off_mspans = o, o = align(o + P.mspans.size() * sizeof(MulTile));
     P.off_ppm = o, o = align(o + P.ppm.size() * sizeof(MulProdTask));
+    P.off_ppg_groups = o, o = align(o + P.ppg_groups.size() * sizeof(MulPPGroup));
+    P.off_ppg_items = o, o = align(o + P.ppg_items.size() * sizeof(MulPPItem));
     P.off_ka_sums = o, o = align(o + P.ka_sums.size() * sizeof(KaSum));
     P.off_ka_vtasks = o, o = align(o + P.ka_vtasks.size() * sizeof(MulVTask));
     P.off_ka_vtiles = o, o = align(o + P.ka_vtiles.size() * sizeof(MulVTile));
@@ -439,6 +481,8 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
     put(P.off_mspans, P.mspans.data(), P.mspans.size() * sizeof(MulTile));
     put(P.off_ppm, P.ppm.data(), P.ppm.size() * sizeof(MulProdTask));
+    put(P.off_ppg_groups, P.ppg_groups.data(), P.ppg_groups.size() * sizeof(MulPPGroup));
+    put(P.off_ppg_items, P.ppg_items.data(), P.ppg_items.size() * sizeof(MulPPItem));
     put(P.off_ka_sums, P.ka_sums.data(), P.ka_sums.size() * sizeof(KaSum));
     put(P.off_ka_vtasks, P.ka_vtasks.data(), P.ka_vtasks.size() * sizeof(MulVTask));
     put(P.off_ka_vtiles, P.ka_vtiles.data(), P.ka_vtiles.size() * sizeof(MulVTile));
@@ -634,6 +678,16 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
         S.B = B, S.a = batch_arg(a), S.b = batch_arg(b), S.K = K;
         fill_bounds(S.ab, a), fill_bounds(S.bb, b);
         if (launch_mul_stage(S, c->stream)) return hip_fail(c, hipGetLastError());
+        if (P->ppg && !P->ppg_groups.empty()) {
+            MulPPGArgs g{};
+            g.B = B;
+            g.groups = (const MulPPGroup *)(T + P->off_ppg_groups);
+            g.items = (const MulPPItem *)(T + P->off_ppg_items);
+            g.ngroups = (uint32_t)P->ppg_groups.size();
+            g.umax = P->ppg_umax, g.vmax = P->ppg_vmax, g.span = P->ppg_span;
+            g.wave_words = mul_mfma_wave_words(g.vmax, g.span, g.umax);
+            if (launch_mul_ppg(g, c->stream)) return hip_fail(c, hipGetLastError());
+        }
         for (uint32_t i = 0; i < K; ++i) {
             const MulPlan::Col &col = P->cols[i];
             MulPPArgs pp{};

@@ -90,23 +90,64 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
     }
 }
 
-// One group of G chunks from c0 over the tiles tlo .. thi of the span
+// The A fragments of chunks c0 .. c0 + G - 1 from the U image RS (R words)
 template <int G>
-__device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
-                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
+__device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int c0, v8i (&Af)[G]) {
     const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
     const int jb = 32 * (R - D + h) - 1 - col;
     const uint32_t *rw0 = RS + (jb >> 3) + 8 * c0;
     const uint32_t sh = 4u * (uint32_t)(jb & 7);
-    v8i Af[G];
 #pragma unroll
     for (int c = 0; c < G; ++c) Af[c] = a_fragment(rw0 + 8 * c, sh);
+}
+
+// Every tile of the span Ts .. Te - 1 that the group of G chunks from c0 reaches
+template <int G>
+__device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI, int vlo, int D,
+                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
     // tiles whose windows (words 32T - D + 2c0 .. 32T + 31 - D + 2(c0 + G) - 1) meet [0, nv)
     const int tlo = max(Ts, floor_div32(D - 2 * c0 - 2 * G + 1));
     const int thi = min(Te - 1, floor_div32(nv - 1 + D - 2 * c0));
     int T = tlo;
     for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT);
     if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
+}
+
+// One group of G chunks from c0 over the tiles tlo .. thi of the span
+template <int G>
+__device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
+                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
+    v8i Af[G];
+    mf_afrags<G>(RS, R, D, c0, Af);
+    mf_sweep<G>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
+}
+
+// RS quad R-1-q = the nibbles of bitreverse(U[q]) for q < ub, zero up to R, then zero to rs_words
+__device__ __forceinline__ void mf_u_image(const uint32_t *U, int ub, int R, uint32_t rs_words,
+                                           const uint32_t *tab, uint32_t *RS) {
+    const int lane = lane_id();
+    for (int q = lane; q < R; q += kWave) {
+        const uint32_t rev = q < ub ? __builtin_bitreverse32(U[q]) : 0u;
+        uint4 x;
+        x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
+        x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
+        ((uint4 *)RS)[R - 1 - q] = x;
+    }
+    for (int k = 4 * R + lane; k < (int)rs_words; k += kWave) RS[k] = 0u;
+}
+
+// VI quad i = the nibbles of V word vlo + i (zero outside [0, nv)) for i < vhi - vlo
+__device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, int vhi,
+                                           const uint32_t *tab, uint32_t *VI) {
+    const int lane = lane_id();
+    for (int i = lane; i < vhi - vlo; i += kWave) {
+        const int w = vlo + i;
+        const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
+        uint4 q;
+        q.x = tab[v & 0xFFu], q.y = tab[(v >> 8) & 0xFFu];
+        q.z = tab[(v >> 16) & 0xFFu], q.w = tab[v >> 24];
+        ((uint4 *)VI)[i] = q;
+    }
 }
 
 template <bool LEAF>
@@ -172,22 +213,8 @@ mul_mfma_kernel(MulMfmaArgs P) {
         const int vhi = min(32 * Te + 32 - D + 2 * nc, nv + kVPad);
         wsync(); // the previous block's reads of RS / VI are done
         // RS quad R-1-q = the nibbles of bitreverse(U_b[q]) (one load, one 16-B store per word)
-        for (int q = lane; q < R; q += kWave) {
-            const uint32_t rev = q < ub ? __builtin_bitreverse32(U[b0 + q]) : 0u;
-            uint4 x;
-            x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
-            x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
-            ((uint4 *)RS)[R - 1 - q] = x;
-        }
-        for (int k = 4 * R + lane; k < (int)rs_words; k += kWave) RS[k] = 0u;
-        for (int i = lane; i < vhi - vlo; i += kWave) {
-            const int w = vlo + i;
-            const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
-            uint4 q;
-            q.x = tab[v & 0xFFu], q.y = tab[(v >> 8) & 0xFFu];
-            q.z = tab[(v >> 16) & 0xFFu], q.w = tab[v >> 24];
-            ((uint4 *)VI)[i] = q;
-        }
+        mf_u_image(U + b0, ub, R, rs_words, tab, RS);
+        mf_v_image(V, nv, vlo, vhi, tab, VI);
         wsync();
         const int tlo = max(Ts, 0);
         uint32_t *OUTs = OUT + 32 * (tlo - Ts);
@@ -209,6 +236,93 @@ mul_mfma_kernel(MulMfmaArgs P) {
     }
     wsync();
     for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
+}
+
+// Partial products a_j * b_k grouped by a_j (MulPPGroup): one wave per (value, group).  a_j has
+// at most kMfPPGWords words, so its chunks (nu/2 + 1 <= 17) are one group: the A fragments are
+// built once, then every product of the group gets its V image, its tiles (the whole output:
+// span tiles) and its output words and degree.  Same products as mul_mfma_kernel<false>.
+template <int G>
+__device__ __forceinline__ void ppg_products(const MulPPGArgs &P, uint64_t e, const MulPPGroup &grp,
+                                             const uint32_t *RS, int nu, uint32_t du,
+                                             const uint32_t *tab, uint32_t *VI, uint32_t *OUT) {
+    const int lane = lane_id();
+    uint32_t *arena = P.B.arena + e * P.B.astride;
+    const int D = nu, R = nu + 2;
+    v8i Af[G];
+    mf_afrags<G>(RS, R, D, 0, Af);
+    for (uint32_t it = 0; it < grp.count; ++it) {
+        const MulPPItem item = P.items[grp.first + it];
+        const uint32_t dv = rfl(P.B.deg1[(uint64_t)item.v * P.B.nv + e]);
+        const int nv = bitwords((int)dv);
+        uint32_t *O = arena + P.B.slots[item.out].off;
+        const int nout = (int)P.B.slots[item.out].words;
+        if (lane == 0) P.B.deg1[(uint64_t)item.out * P.B.nv + e] = dv ? du + dv - 1 : 0u;
+        if (nv == 0) {
+            for (int w = lane; w < nout; w += kWave) O[w] = 0u;
+            continue;
+        }
+        const int Te = min((int)P.span, (nout + 31) >> 5);
+        const int vlo = max(-D, -kVPad);
+        const int vhi = min(32 * Te + 32 - D + 2 * G, nv + kVPad);
+        wsync(); // the previous product's reads of VI and OUT are done
+        mf_v_image(arena + P.B.slots[item.v].off, nv, vlo, vhi, tab, VI);
+        for (int w = lane; w < nout; w += kWave) OUT[w] = 0u;
+        wsync();
+        mf_sweep<G>(Af, VI, vlo, D, nv, 0, Te, 0, OUT);
+        wsync();
+        for (int w = lane; w < nout; w += kWave) O[w] = OUT[w];
+    }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HM_MF_WPE_MIN, HM_MF_WPE)))
+mul_ppg_kernel(MulPPGArgs P) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *tab = lds;
+    nibble_table(tab);
+    __syncthreads();
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint64_t e = g / P.ngroups;
+    if (e >= P.B.nv) return; // whole wave exits together
+    const MulPPGroup grp = P.groups[g % P.ngroups];
+    const int lane = lane_id();
+    uint32_t *arena = P.B.arena + e * P.B.astride;
+    const uint32_t du = rfl(P.B.deg1[(uint64_t)grp.u * P.B.nv + e]);
+    const int nu = bitwords((int)du);
+    if (nu == 0 || nu > (int)kMfPPGWords) { // null a_j: every product of the group is null
+        for (uint32_t it = 0; it < grp.count; ++it) {
+            const MulPPItem item = P.items[grp.first + it];
+            uint32_t *O = arena + P.B.slots[item.out].off;
+            for (int w = lane; w < (int)P.B.slots[item.out].words; w += kWave) O[w] = 0u;
+            if (lane == 0) P.B.deg1[(uint64_t)item.out * P.B.nv + e] = 0u;
+        }
+        if (nu > (int)kMfPPGWords && lane == 0) flag(P.B.status, HM_ERR_BAD_INPUT); // (plan bound)
+        return;
+    }
+    uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
+    const uint32_t rs_words = mf_rs_words(P.umax);
+    uint32_t *VI = RS + rs_words;
+    uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
+    mf_u_image(arena + P.B.slots[grp.u].off, nu, nu + 2, rs_words, tab, RS);
+    wsync();
+    switch (nu / 2 + 1) {
+#define HM_PPG(G) \
+    case G: ppg_products<G>(P, e, grp, RS, nu, du, tab, VI, OUT); break;
+        HM_PPG(1) HM_PPG(2) HM_PPG(3) HM_PPG(4) HM_PPG(5) HM_PPG(6) HM_PPG(7) HM_PPG(8) HM_PPG(9)
+        HM_PPG(10) HM_PPG(11) HM_PPG(12) HM_PPG(13) HM_PPG(14) HM_PPG(15) HM_PPG(16) HM_PPG(17)
+#undef HM_PPG
+    default: break;
+    }
+}
+
+int launch_mul_ppg(const MulPPGArgs &a, void *stream) {
+    const uint64_t waves = a.B.nv * a.ngroups;
+    if (!waves) return 0;
+    const size_t lds = (256 + (size_t)a.wave_words * 4) * 4;
+    hipLaunchKernelGGL(mul_ppg_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+                       (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
