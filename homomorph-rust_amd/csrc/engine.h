@@ -180,6 +180,17 @@ struct MulVProdArgs {
 // explicit span list {task, first output word}); vmax = the largest V of the launch (words).
 constexpr int kMfUB = 256;
 constexpr int kMfSpan = 16;
+// the narrow class of schoolbook carries: U of at most kMfNarrowWords words, launched apart from
+// the wide ones (mul_mfma_kernel<false, true>: 4 waves per SIMD), spans of at most kMfNarrowSpan
+// tiles so that 16 waves' LDS slices fit a CU
+#ifndef HM_MF_NARROW_WORDS
+#define HM_MF_NARROW_WORDS 72
+#endif
+#ifndef HM_MF_NARROW_SPAN
+#define HM_MF_NARROW_SPAN 10
+#endif
+constexpr uint32_t kMfNarrowWords = HM_MF_NARROW_WORDS;
+constexpr uint32_t kMfNarrowSpan = HM_MF_NARROW_SPAN;
 struct MulMfmaArgs {
     MulBase B;
     const void *tasks;
@@ -194,6 +205,8 @@ struct MulMfmaArgs {
 // a_j * b_k of the plan in one launch before the columns, one wave per (value, a_j), a_j's A
 // fragments built once for all of its products (a_j within kMfPPGWords words: one chunk group).
 constexpr uint32_t kMfPPGWords = 34;
+// b_k words staged per batch of partial products (mul_ppg_kernel: kMfPPGBatch x 64 LDS words)
+constexpr uint32_t kMfPPGBatch = 8;
 struct MulPPGroup {
     uint32_t u;            // slot of a_j (the shared factor)
     uint32_t first, count; // its products: items [first, first + count)

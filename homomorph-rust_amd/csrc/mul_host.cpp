@@ -62,11 +62,6 @@ struct MfLaunch {
     uint32_t spans = 0, nspans = 0; // MulTile range in mspans
     uint32_t vmax = 0, umax = 0, span = 0;
 };
-// shorter operand (words) of the narrow class of schoolbook carries
-#ifndef HM_MF_NARROW_WORDS
-#define HM_MF_NARROW_WORDS 72
-#endif
-constexpr uint32_t kMfNarrowWords = HM_MF_NARROW_WORDS;
 
 struct MulPlan {
     // key
@@ -416,7 +411,7 @@ bool build_plan(MulPlan &P) {
         }
         for (int cl = 0; cl < 2; ++cl) {
             MfLaunch &m = col.mfl[cl];
-            m.span = std::min<uint32_t>(kMfSpan, std::max<uint32_t>(1, (omax[cl] + 31) / 32));
+            m.span = std::min<uint32_t>(cl ? kMfSpan : kMfNarrowSpan, std::max<uint32_t>(1, (omax[cl] + 31) / 32));
             m.spans = (uint32_t)P.mspans.size();
             for (uint32_t k : mfk[cl])
                 for (uint32_t base = 0; base < P.slots[P.prod[k].out].words; base += 32 * m.span)
@@ -685,7 +680,7 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             g.items = (const MulPPItem *)(T + P->off_ppg_items);
             g.ngroups = (uint32_t)P->ppg_groups.size();
             g.umax = P->ppg_umax, g.vmax = P->ppg_vmax, g.span = P->ppg_span;
-            g.wave_words = mul_mfma_wave_words(g.vmax, g.span, g.umax);
+            g.wave_words = mul_mfma_wave_words(g.vmax, g.span, g.umax) + 64 * kMfPPGBatch;
             if (launch_mul_ppg(g, c->stream)) return hip_fail(c, hipGetLastError());
         }
         for (uint32_t i = 0; i < K; ++i) {

@@ -101,25 +101,30 @@ __device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int 
     for (int c = 0; c < G; ++c) Af[c] = a_fragment(rw0 + 8 * c, sh);
 }
 
-// Every tile of the span Ts .. Te - 1 that the group of G chunks from c0 reaches
-template <int G>
+// Every tile of the span Ts .. Te - 1 that the group of G chunks from c0 reaches: two tiles at a
+// time (two accumulator chains), or (PAIRS false: 16 + 12 fewer VGPRs) one at a time
+template <int G, bool PAIRS = true>
 __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI, int vlo, int D,
                                          int nv, int Ts, int Te, int c0, uint32_t *OUT) {
     // tiles whose windows (words 32T - D + 2c0 .. 32T + 31 - D + 2(c0 + G) - 1) meet [0, nv)
     const int tlo = max(Ts, floor_div32(D - 2 * c0 - 2 * G + 1));
     const int thi = min(Te - 1, floor_div32(nv - 1 + D - 2 * c0));
     int T = tlo;
-    for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT);
-    if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
+    if constexpr (PAIRS) {
+        for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT);
+        if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
+    } else {
+        for (; T <= thi; ++T) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
+    }
 }
 
 // One group of G chunks from c0 over the tiles tlo .. thi of the span
-template <int G>
+template <int G, bool PAIRS = true>
 __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
                                          int nv, int Ts, int Te, int c0, uint32_t *OUT) {
     v8i Af[G];
     mf_afrags<G>(RS, R, D, c0, Af);
-    mf_sweep<G>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
+    mf_sweep<G, PAIRS>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
 }
 
 // RS quad R-1-q = the nibbles of bitreverse(U[q]) for q < ub, zero up to R, then zero to rs_words
@@ -150,14 +155,22 @@ __device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, i
     }
 }
 
-template <bool LEAF>
 #ifndef HM_MF_WPE
 #define HM_MF_WPE 3
 #endif
 #ifndef HM_MF_WPE_MIN
 #define HM_MF_WPE_MIN 2
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HM_MF_WPE_MIN, HM_MF_WPE)))
+#ifndef HM_MFN_WPE
+#define HM_MFN_WPE 4
+#endif
+// NARROW: the launches whose U has at most kMfNarrowWords words (mul_host.cpp).  Such a wave is
+// short (a 33-word U is 17 chunks: ~76 MFMAs) and waits on its record and operand loads for much
+// of its life, so this instance trades the paired tile chains for occupancy: one tile at a time,
+// <= 128 VGPRs, 4 waves per SIMD (the host sizes the narrow spans so 16 waves' LDS slices fit).
+template <bool LEAF, bool NARROW = false>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(NARROW ? HM_MFN_WPE : HM_MF_WPE_MIN, NARROW ? HM_MFN_WPE : HM_MF_WPE)))
 mul_mfma_kernel(MulMfmaArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
@@ -223,10 +236,11 @@ mul_mfma_kernel(MulMfmaArgs P) {
         // 17-word partial products at d + d' = 512: 9 chunks) takes one gather per tile instead of
         // one per 4-chunk group, and a 256-word leaf's 129 chunks end in a 17-chunk group
         int c0 = 0;
-        for (; nc - c0 > kMfG + 1; c0 += kMfG) mf_group<kMfG>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        for (; nc - c0 > kMfG + 1; c0 += kMfG)
+            mf_group<kMfG, !NARROW>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
         switch (nc - c0) {
 #define HM_MF_TAIL(G) \
-    case G: mf_group<G>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs); break;
+    case G: mf_group<G, !NARROW>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs); break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
             HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)
             HM_MF_TAIL(13) HM_MF_TAIL(14) HM_MF_TAIL(15) HM_MF_TAIL(16) HM_MF_TAIL(17)
@@ -242,36 +256,73 @@ mul_mfma_kernel(MulMfmaArgs P) {
 // at most kMfPPGWords words, so its chunks (nu/2 + 1 <= 17) are one group: the A fragments are
 // built once, then every product of the group gets its V image, its tiles (the whole output:
 // span tiles) and its output words and degree.  Same products as mul_mfma_kernel<false>.
+// A product is only 2 x (nu/2 + 1) MFMAs, so its loads are staged per batch of kPPGBatch items
+// instead of per product: the items' records (one lane each), then their degrees and slots, then
+// every item's b_k words into the wave's VW slice (one word per lane and item, all in flight
+// together) -- three dependent loads per batch where a product at a time took three each.
+constexpr int kPPGBatch = (int)kMfPPGBatch;
+static_assert(kMfPPGWords <= 64, "one word per lane");
+
 template <int G>
 __device__ __forceinline__ void ppg_products(const MulPPGArgs &P, uint64_t e, const MulPPGroup &grp,
                                              const uint32_t *RS, int nu, uint32_t du,
-                                             const uint32_t *tab, uint32_t *VI, uint32_t *OUT) {
+                                             const uint32_t *tab, uint32_t *VW, uint32_t *VI,
+                                             uint32_t *OUT) {
     const int lane = lane_id();
     uint32_t *arena = P.B.arena + e * P.B.astride;
     const int D = nu, R = nu + 2;
+    const int vlo = -D; // D <= kMfPPGWords < kVPad
     v8i Af[G];
     mf_afrags<G>(RS, R, D, 0, Af);
-    for (uint32_t it = 0; it < grp.count; ++it) {
-        const MulPPItem item = P.items[grp.first + it];
-        const uint32_t dv = rfl(P.B.deg1[(uint64_t)item.v * P.B.nv + e]);
-        const int nv = bitwords((int)dv);
-        uint32_t *O = arena + P.B.slots[item.out].off;
-        const int nout = (int)P.B.slots[item.out].words;
-        if (lane == 0) P.B.deg1[(uint64_t)item.out * P.B.nv + e] = dv ? du + dv - 1 : 0u;
-        if (nv == 0) {
-            for (int w = lane; w < nout; w += kWave) O[w] = 0u;
-            continue;
+    for (uint32_t i0 = 0; i0 < grp.count; i0 += kPPGBatch) {
+        const int nb = (int)min((uint32_t)kPPGBatch, grp.count - i0);
+        uint32_t dv = 0u, voff = 0u, ooff = 0u, ow = 0u, oslot = 0u;
+        if (lane < nb) {
+            const MulPPItem it = P.items[grp.first + i0 + lane];
+            dv = P.B.deg1[(uint64_t)it.v * P.B.nv + e];
+            voff = P.B.slots[it.v].off;
+            ooff = P.B.slots[it.out].off;
+            ow = P.B.slots[it.out].words;
+            oslot = it.out;
         }
-        const int Te = min((int)P.span, (nout + 31) >> 5);
-        const int vlo = max(-D, -kVPad);
-        const int vhi = min(32 * Te + 32 - D + 2 * G, nv + kVPad);
-        wsync(); // the previous product's reads of VI and OUT are done
-        mf_v_image(arena + P.B.slots[item.v].off, nv, vlo, vhi, tab, VI);
-        for (int w = lane; w < nout; w += kWave) OUT[w] = 0u;
-        wsync();
-        mf_sweep<G>(Af, VI, vlo, D, nv, 0, Te, 0, OUT);
-        wsync();
-        for (int w = lane; w < nout; w += kWave) O[w] = OUT[w];
+        uint32_t vw[kPPGBatch];
+#pragma unroll
+        for (int k = 0; k < kPPGBatch; ++k) {
+            const int nvk = bitwords((int)__builtin_amdgcn_readlane(dv, k));
+            const uint32_t vo = __builtin_amdgcn_readlane(voff, k);
+            vw[k] = (k < nb && lane < nvk) ? arena[vo + lane] : 0u;
+        }
+        wsync(); // the previous batch's reads of VW are done
+#pragma unroll
+        for (int k = 0; k < kPPGBatch; ++k) VW[64 * k + lane] = vw[k];
+        for (int k = 0; k < nb; ++k) {
+            const uint32_t dvk = __builtin_amdgcn_readlane(dv, k);
+            const int nv = bitwords((int)dvk);
+            uint32_t *O = arena + __builtin_amdgcn_readlane(ooff, k);
+            const int nout = (int)__builtin_amdgcn_readlane(ow, k);
+            if (lane == 0)
+                P.B.deg1[(uint64_t)__builtin_amdgcn_readlane(oslot, k) * P.B.nv + e] = dvk ? du + dvk - 1 : 0u;
+            if (nv == 0) {
+                for (int w = lane; w < nout; w += kWave) O[w] = 0u;
+                continue;
+            }
+            const int Te = min((int)P.span, (nout + 31) >> 5);
+            const int vhi = min(32 * Te + 32 - D + 2 * G, nv + kVPad);
+            wsync(); // VW written; the previous product's reads of VI and OUT are done
+            for (int j = lane; j < vhi - vlo; j += kWave) {
+                const int w = vlo + j;
+                const uint32_t v = (w >= 0 && w < nv) ? VW[64 * k + w] : 0u;
+                uint4 q;
+                q.x = tab[v & 0xFFu], q.y = tab[(v >> 8) & 0xFFu];
+                q.z = tab[(v >> 16) & 0xFFu], q.w = tab[v >> 24];
+                ((uint4 *)VI)[j] = q;
+            }
+            for (int w = lane; w < nout; w += kWave) OUT[w] = 0u;
+            wsync();
+            mf_sweep<G>(Af, VI, vlo, D, nv, 0, Te, 0, OUT);
+            wsync();
+            for (int w = lane; w < nout; w += kWave) O[w] = OUT[w];
+        }
     }
 }
 
@@ -304,11 +355,12 @@ mul_ppg_kernel(MulPPGArgs P) {
     const uint32_t rs_words = mf_rs_words(P.umax);
     uint32_t *VI = RS + rs_words;
     uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
+    uint32_t *VW = OUT + 32 * P.span; // kPPGBatch x 64 staged b_k words
     mf_u_image(arena + P.B.slots[grp.u].off, nu, nu + 2, rs_words, tab, RS);
     wsync();
     switch (nu / 2 + 1) {
 #define HM_PPG(G) \
-    case G: ppg_products<G>(P, e, grp, RS, nu, du, tab, VI, OUT); break;
+    case G: ppg_products<G>(P, e, grp, RS, nu, du, tab, VW, VI, OUT); break;
         HM_PPG(1) HM_PPG(2) HM_PPG(3) HM_PPG(4) HM_PPG(5) HM_PPG(6) HM_PPG(7) HM_PPG(8) HM_PPG(9)
         HM_PPG(10) HM_PPG(11) HM_PPG(12) HM_PPG(13) HM_PPG(14) HM_PPG(15) HM_PPG(16) HM_PPG(17)
 #undef HM_PPG
@@ -331,6 +383,8 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
     const size_t lds = (256 + (size_t)a.wave_words * 4) * 4;
     const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
     if (leaf) hipLaunchKernelGGL(mul_mfma_kernel<true>, grid, block, lds, (hipStream_t)stream, a);
+    else if (a.umax <= kMfNarrowWords)
+        hipLaunchKernelGGL((mul_mfma_kernel<false, true>), grid, block, lds, (hipStream_t)stream, a);
     else hipLaunchKernelGGL(mul_mfma_kernel<false>, grid, block, lds, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
