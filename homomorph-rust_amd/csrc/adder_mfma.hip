@@ -64,10 +64,15 @@ __device__ unsigned long long *g_mfma_prof; // 4 per wave, set by the harness
 #ifndef HM_MFMA_PREFETCH
 #define HM_MFMA_PREFETCH 3
 #endif
-constexpr int kPrefetch = HM_MFMA_PREFETCH;
+// the 25-chunk chain (2 waves per SIMD, VGPRs to spare) reads 4 ahead: configs[4] 925-929 ->
+// 922-923 ms per 2^20 (2: 932-936, 5: 926-927)
+#ifndef HM_MFMA_PREFETCH25
+#define HM_MFMA_PREFETCH25 4
+#endif
+template <int NC> constexpr int kPrefetchOf = NC > 16 ? HM_MFMA_PREFETCH25 : HM_MFMA_PREFETCH;
 // side(k) runs after MFMA k for k = 1, 4, 7 (the next tile's ring fill in three stages: its LDS
 // latency hides under this tile's MFMAs instead of stalling the wave between tiles)
-template <int NC, class Side>
+template <int NC, class Side, int kPrefetch = kPrefetchOf<NC>>
 __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[NC], const uint4 *rb, const uint4 *rbn,
                                           uint4 (&pf)[kPrefetch], v16f acc, Side &&side) {
     // pf holds this tile's first kPrefetch B fragments (read during the tile before); the last
@@ -307,6 +312,7 @@ add_chain_mfma_kernel(AddArgs A) {
             return (const uint4 *)&ring[((32 * T + col - D + h) & (kMfmaRingSlots - 1)) * 4];
         };
         wsync(); // the first tile's ring images are written
+        constexpr int kPrefetch = kPrefetchOf<NC>;
         uint4 pf[kPrefetch];
 #pragma unroll
         for (int c = 0; c < kPrefetch; ++c) pf[c] = rbase(tiles - 1)[2 * c];

@@ -191,6 +191,10 @@ constexpr int kMfSpan = 16;
 #endif
 constexpr uint32_t kMfNarrowWords = HM_MF_NARROW_WORDS;
 constexpr uint32_t kMfNarrowSpan = HM_MF_NARROW_SPAN;
+#ifndef HM_MF_WIDE_SPAN
+#define HM_MF_WIDE_SPAN 16
+#endif
+constexpr uint32_t kMfWideSpan = HM_MF_WIDE_SPAN; // tiles per wave of the wide class
 struct MulMfmaArgs {
     MulBase B;
     const void *tasks;

@@ -323,34 +323,40 @@ int launch_mul_vprod(const MulVProdArgs &P, uint32_t w, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// r[0:min(4h, rcap)) = z0 + (z0 + z1 + z2) X^h + z1 X^2h  (z* are 2h words; X^h = h words)
+// r[0:min(4h, rcap)) = z0 + (z0 + z1 + z2) X^h + z1 X^2h  (z* are 2h words; X^h = h words).
+// One lane per 4-word offset o of the half: it reads z0, z1, z2 at o and h + o once each and
+// writes r at o, h + o, 2h + o, 3h + o (10h words of traffic; a lane per output word re-read the
+// middle terms: 14h)
 __global__ void __launch_bounds__(256) ka_comb_kernel(KaCombArgs A) {
     const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rfl(threadIdx.x >> 6);
-    const uint32_t h = A.h, chunks = (4 * h + 255) / 256;
+    const uint32_t h = A.h, chunks = (h + 255) / 256;
     const uint64_t per_value = (uint64_t)A.nt * chunks;
     const uint64_t e = g / per_value;
     if (e >= A.B.nv) return;
     const uint32_t r = (uint32_t)(g % per_value);
     const KaComb t = A.t[r / chunks];
-    const uint32_t w = (r % chunks) * 256 + 4u * (uint32_t)lane_id();
-    if (w >= 4 * h || w >= t.rcap) return;
+    const uint32_t o = (r % chunks) * 256 + 4u * (uint32_t)lane_id();
+    if (o >= h || o >= t.rcap) return;
     uint32_t *base = A.B.arena + e * A.B.astride;
     const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
     auto ld = [&](uint32_t off, uint32_t i) -> uint4 {
         return off == kKaNone ? zero : *(const uint4 *)(base + off + i);
     };
     auto x = [](uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); };
-    const uint32_t seg = w / h, o = w % h;
-    uint4 v;
-    if (seg == 0) v = ld(t.z0, o);
-    else if (seg == 1) v = x(x(ld(t.z0, h + o), ld(t.z0, o)), x(ld(t.z1, o), ld(t.z2, o)));
-    else if (seg == 2) v = x(x(ld(t.z1, o), ld(t.z0, h + o)), x(ld(t.z1, h + o), ld(t.z2, h + o)));
-    else v = ld(t.z1, h + o);
-    *(uint4 *)(base + t.r + w) = v;
+    const bool s1 = h + o < t.rcap, s2 = 2 * h + o < t.rcap, s3 = 3 * h + o < t.rcap;
+    const uint4 a0 = ld(t.z0, o);
+    uint4 a1 = zero, b0 = zero, c0 = zero, b1 = zero, c1 = zero;
+    if (s1) a1 = ld(t.z0, h + o), b0 = ld(t.z1, o), c0 = ld(t.z2, o);
+    if (s2) b1 = ld(t.z1, h + o), c1 = ld(t.z2, h + o);
+    uint4 *R = (uint4 *)(base + t.r + o);
+    R[0] = a0;
+    if (s1) *(uint4 *)(base + t.r + h + o) = x(x(a0, a1), x(b0, c0));
+    if (s2) *(uint4 *)(base + t.r + 2 * h + o) = x(x(b0, a1), x(b1, c1));
+    if (s3) *(uint4 *)(base + t.r + 3 * h + o) = b1;
 }
 
 int launch_ka_comb(const KaCombArgs &A, void *stream) {
-    const uint64_t waves = A.B.nv * A.nt * ((4 * A.h + 255) / 256);
+    const uint64_t waves = A.B.nv * A.nt * ((A.h + 255) / 256);
     if (!waves) return 0;
     hipLaunchKernelGGL(ka_comb_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, A);

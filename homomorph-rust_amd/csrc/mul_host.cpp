@@ -411,7 +411,7 @@ bool build_plan(MulPlan &P) {
         }
         for (int cl = 0; cl < 2; ++cl) {
             MfLaunch &m = col.mfl[cl];
-            m.span = std::min<uint32_t>(cl ? kMfSpan : kMfNarrowSpan, std::max<uint32_t>(1, (omax[cl] + 31) / 32));
+            m.span = std::min<uint32_t>(cl ? kMfWideSpan : kMfNarrowSpan, std::max<uint32_t>(1, (omax[cl] + 31) / 32));
             m.spans = (uint32_t)P.mspans.size();
             for (uint32_t k : mfk[cl])
                 for (uint32_t base = 0; base < P.slots[P.prod[k].out].words; base += 32 * m.span)
