@@ -195,6 +195,14 @@ constexpr uint32_t kMfNarrowSpan = HM_MF_NARROW_SPAN;
 #define HM_MF_WIDE_SPAN 16
 #endif
 constexpr uint32_t kMfWideSpan = HM_MF_WIDE_SPAN; // tiles per wave of the wide class
+// Karatsuba leaves of at most kMfLeanLeafWords words run on mul_mfma_kernel<true, true> (per-group
+// U windows, one tile at a time, 4 waves per SIMD): configs[4]'s 224-word leaves 916-919 -> 911-913
+// ms per 2^20; K = 16's 256-word leaves measured 0.5 % slower on it (336-338 -> 338-339 ms), so
+// they stay on the 3-wave instance
+#ifndef HM_MF_LEAN_LEAF_WORDS
+#define HM_MF_LEAN_LEAF_WORDS 224
+#endif
+constexpr uint32_t kMfLeanLeafWords = HM_MF_LEAN_LEAF_WORDS;
 struct MulMfmaArgs {
     MulBase B;
     const void *tasks;
@@ -204,6 +212,7 @@ struct MulMfmaArgs {
     uint32_t span;        // output tiles per span
     uint32_t vmax, wave_words;
     uint32_t umax;        // largest U (words; blocks of at most kMfUB): sizes the U image
+    uint32_t lean;        // leaves: the lean instance (per-group U windows, 4 waves per SIMD)
 };
 // Partial products grouped by their shared factor a_j (mul_mfma.hip mul_ppg_kernel): every
 // a_j * b_k of the plan in one launch before the columns, one wave per (value, a_j), a_j's A
@@ -294,6 +303,7 @@ int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
 int launch_mul_ppg(const MulPPGArgs &a, void *stream);
 uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
+uint32_t mul_mfma_lean_leaf_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);
 int launch_mul_deg(const MulDegArgs &a, void *stream);
 constexpr uint32_t kMulTileW[] = {1, 2, 4, 8, 12}; // per-lane tile widths of the product launches

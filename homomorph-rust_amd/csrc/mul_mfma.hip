@@ -155,6 +155,40 @@ __device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, i
     }
 }
 
+// One group of G chunks from c0 whose A fragments come from a window of the U image built for
+// this group alone (the lean leaf instance keeps no whole-U image): RS quads Qlo = 2 c0 + 1 ..
+// Qlo + 2G + 1, i.e. U words q = R - 1 - Q (zero outside [0, ub)), are all its fragments read
+__host__ __device__ constexpr uint32_t mf_win_words(int G) { return 4u * (2u * (uint32_t)G + 2u) + 16u; }
+// lane k's U word of the window of the group of G chunks from c0 (k < 2G + 2 <= 36 lanes)
+__device__ __forceinline__ uint32_t mf_win_word(const uint32_t *Ub, int ub, int R, int c0, int G) {
+    const int lane = lane_id();
+    const int q = R - 1 - (2 * c0 + 1 + lane);
+    return (lane < 2 * G + 2 && q >= 0 && q < ub) ? Ub[q] : 0u;
+}
+// wword: this lane's window word (mf_win_word, loaded ahead); the next group's is loaded here,
+// before the sweep, into *next (G2 chunks from c0 + G; G2 = 0: none)
+template <int G>
+__device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub, int ub, int G2,
+                                             uint32_t *next, uint32_t *RSW, const uint32_t *tab,
+                                             const uint32_t *VI, int vlo, int R, int D, int nv,
+                                             int Ts, int Te, int c0, uint32_t *OUT) {
+    const int lane = lane_id();
+    const int Qlo = 2 * c0 + 1;
+    wsync(); // the previous group's fragment reads are done
+    if (lane < 2 * G + 2) {
+        const uint32_t rev = __builtin_bitreverse32(wword);
+        uint4 x;
+        x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
+        x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
+        ((uint4 *)RSW)[lane] = x;
+    }
+    wsync();
+    v8i Af[G];
+    mf_afrags<G>(RSW - 4 * Qlo, R, D, c0, Af);
+    if (G2) *next = mf_win_word(Ub, ub, R, c0 + G, G2);
+    mf_sweep<G, false>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
+}
+
 #ifndef HM_MF_WPE
 #define HM_MF_WPE 3
 #endif
@@ -164,13 +198,16 @@ __device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, i
 #ifndef HM_MFN_WPE
 #define HM_MFN_WPE 4
 #endif
-// NARROW: the launches whose U has at most kMfNarrowWords words (mul_host.cpp).  Such a wave is
-// short (a 33-word U is 17 chunks: ~76 MFMAs) and waits on its record and operand loads for much
-// of its life, so this instance trades the paired tile chains for occupancy: one tile at a time,
-// <= 128 VGPRs, 4 waves per SIMD (the host sizes the narrow spans so 16 waves' LDS slices fit).
-template <bool LEAF, bool NARROW = false>
+// LEAN instances trade the paired tile chains for occupancy: one tile at a time, <= 128 VGPRs,
+// 4 waves per SIMD.
+//  - schoolbook (LEAF false): the launches whose U has at most kMfNarrowWords words (mul_host.cpp).
+//    Such a wave is short (a 33-word U is 17 chunks: ~76 MFMAs) and waits on its record and operand
+//    loads for much of its life; the host sizes the narrow spans so 16 waves' LDS slices fit.
+//  - leaves (LEAF true): no whole-U image either, only each group's window (mf_group_win), so a
+//    256-word leaf's LDS slice is ~9 KB instead of ~12.5 KB and 16 waves fit a CU.
+template <bool LEAF, bool LEAN = false>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(NARROW ? HM_MFN_WPE : HM_MF_WPE_MIN, NARROW ? HM_MFN_WPE : HM_MF_WPE)))
+__attribute__((amdgpu_waves_per_eu(LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN, LEAN ? HM_MFN_WPE : HM_MF_WPE)))
 mul_mfma_kernel(MulMfmaArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
@@ -210,8 +247,9 @@ mul_mfma_kernel(MulMfmaArgs P) {
         for (int w = base + lane; w < wend; w += kWave) O[w] = 0u;
         return;
     }
+    constexpr bool WIN = LEAF && LEAN; // per-group U windows instead of the whole U image
     uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
-    const uint32_t rs_words = mf_rs_words(P.umax);
+    const uint32_t rs_words = WIN ? mf_win_words(kMfG + 1) : mf_rs_words(P.umax);
     uint32_t *VI = RS + rs_words;
     uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
     for (int w = lane; w < wend - base; w += kWave) OUT[w] = 0u; // the span's live words
@@ -226,7 +264,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
         const int vhi = min(32 * Te + 32 - D + 2 * nc, nv + kVPad);
         wsync(); // the previous block's reads of RS / VI are done
         // RS quad R-1-q = the nibbles of bitreverse(U_b[q]) (one load, one 16-B store per word)
-        mf_u_image(U + b0, ub, R, rs_words, tab, RS);
+        if constexpr (!WIN) mf_u_image(U + b0, ub, R, rs_words, tab, RS);
         mf_v_image(V, nv, vlo, vhi, tab, VI);
         wsync();
         const int tlo = max(Ts, 0);
@@ -236,11 +274,22 @@ mul_mfma_kernel(MulMfmaArgs P) {
         // 17-word partial products at d + d' = 512: 9 chunks) takes one gather per tile instead of
         // one per 4-chunk group, and a 256-word leaf's 129 chunks end in a 17-chunk group
         int c0 = 0;
-        for (; nc - c0 > kMfG + 1; c0 += kMfG)
-            mf_group<kMfG, !NARROW>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        // (lean leaves) each group's U window words are loaded one group ahead
+        auto gsize = [&](int c) { return nc - c > kMfG + 1 ? kMfG : nc - c; };
+        uint32_t ww = WIN ? mf_win_word(U + b0, ub, R, 0, gsize(0)) : 0u;
+        for (; nc - c0 > kMfG + 1; c0 += kMfG) {
+            if constexpr (WIN)
+                mf_group_win<kMfG>(ww, U + b0, ub, gsize(c0 + kMfG), &ww, RS, tab, VI, vlo, R, D, nv,
+                                   tlo, Te, c0, OUTs);
+            else mf_group<kMfG, !LEAN>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+        }
         switch (nc - c0) {
 #define HM_MF_TAIL(G) \
-    case G: mf_group<G, !NARROW>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs); break;
+    case G:                                                                                      \
+        if constexpr (WIN)                                                                       \
+            mf_group_win<G>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0, OUTs); \
+        else mf_group<G, !LEAN>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);                     \
+        break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
             HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)
             HM_MF_TAIL(13) HM_MF_TAIL(14) HM_MF_TAIL(15) HM_MF_TAIL(16) HM_MF_TAIL(17)
@@ -382,7 +431,9 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
     if (!waves) return 0;
     const size_t lds = (256 + (size_t)a.wave_words * 4) * 4;
     const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
-    if (leaf) hipLaunchKernelGGL(mul_mfma_kernel<true>, grid, block, lds, (hipStream_t)stream, a);
+    if (leaf && a.lean)
+        hipLaunchKernelGGL((mul_mfma_kernel<true, true>), grid, block, lds, (hipStream_t)stream, a);
+    else if (leaf) hipLaunchKernelGGL(mul_mfma_kernel<true>, grid, block, lds, (hipStream_t)stream, a);
     else if (a.umax <= kMfNarrowWords)
         hipLaunchKernelGGL((mul_mfma_kernel<false, true>), grid, block, lds, (hipStream_t)stream, a);
     else hipLaunchKernelGGL(mul_mfma_kernel<false>, grid, block, lds, (hipStream_t)stream, a);
@@ -391,6 +442,10 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
 
 uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax) {
     return mf_wave_words(vmax, span, umax);
+}
+
+uint32_t mul_mfma_lean_leaf_wave_words(uint32_t vmax, uint32_t span, uint32_t umax) {
+    return mf_win_words(kMfG + 1) + mf_vi_words(vmax, span, umax) + 32 * span;
 }
 
 } // namespace hm
