@@ -131,7 +131,7 @@ constexpr int kMfmaWpb = HM_MFMA_WPB;
 static_assert(kMfmaWpb <= kAddWavesPerBlock, "host LDS plan");
 
 // NC = 13: 4 waves per SIMD (configs[1]'s 4096 waves fill the chip at that), 128 VGPRs;
-// NC = 25: 2 waves per SIMD, 256 VGPRs (the 25 A fragments alone are 100)
+// NC = 25: 3 waves per SIMD, 168 VGPRs (the 25 A fragments alone are 100; engine.h HM_MFMA25_WPE)
 template <int NC>
 __global__ void __launch_bounds__(64 * kMfmaWpb)
 __attribute__((amdgpu_waves_per_eu(MfmaCfg<NC>::kWavesPerEU, MfmaCfg<NC>::kWavesPerEU)))

@@ -333,7 +333,12 @@ template <int NC> struct MfmaCfg {
     static constexpr int kRsWords = 4 * kRevWords + 8 * NC + 8;
     static constexpr int kHalo = NC <= 16 ? 32 : 64;        // >= 2 NC - 1
     static constexpr int kRecWords = NC <= 16 ? 64 : 128;
-    static constexpr int kWavesPerEU = NC <= 16 ? 4 : 2;
+// NC = 25: 3 waves per SIMD (168 VGPRs; 23 dwords spill, all outside the tile loop): configs[4]
+// 910.5-911.9 -> 902.8-905.1 ms per 2^20 against 2 waves per SIMD at 197 VGPRs (round 4)
+#ifndef HM_MFMA25_WPE
+#define HM_MFMA25_WPE 3
+#endif
+    static constexpr int kWavesPerEU = NC <= 16 ? 4 : HM_MFMA25_WPE;
     static constexpr int kStageWords = 2 * kRecWords * kAddWavesPerBlock; // static LDS per block
     // ring slots mirrored past the end (slot s < kMirror also at kMfmaRingSlots + s), so every
     // lane's window of 2 NC - 1 slots is contiguous wherever it starts
