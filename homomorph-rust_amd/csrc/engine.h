@@ -195,6 +195,12 @@ constexpr uint32_t kMfNarrowSpan = HM_MF_NARROW_SPAN;
 #define HM_MF_WIDE_SPAN 16
 #endif
 constexpr uint32_t kMfWideSpan = HM_MF_WIDE_SPAN; // tiles per wave of the wide class
+// the wide class on the lean windowed instance (mul_mfma_kernel<false, true, true>): configs[4]
+// 897.7-901.0 -> 895.4-895.5 ms per 2^20 (spans of 12 tiles: 899-904, 8: 908-909)
+#ifndef HM_MF_WIDE_LEAN
+#define HM_MF_WIDE_LEAN 1
+#endif
+constexpr bool kMfWideLean = HM_MF_WIDE_LEAN;
 // Karatsuba leaves of at most kMfLeanLeafWords words run on mul_mfma_kernel<true, true> (per-group
 // U windows, one tile at a time, 4 waves per SIMD): configs[4]'s 224-word leaves 916-919 -> 911-913
 // ms per 2^20; K = 16's 256-word leaves measured 0.5 % slower on it (336-338 -> 338-339 ms), so

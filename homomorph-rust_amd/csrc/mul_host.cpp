@@ -61,6 +61,7 @@ struct KaProg {
 struct MfLaunch {
     uint32_t spans = 0, nspans = 0; // MulTile range in mspans
     uint32_t vmax = 0, umax = 0, span = 0;
+    bool lean = false; // wide class on the lean windowed instance
 };
 
 struct MulPlan {
@@ -411,7 +412,9 @@ bool build_plan(MulPlan &P) {
         }
         for (int cl = 0; cl < 2; ++cl) {
             MfLaunch &m = col.mfl[cl];
-            m.span = std::min<uint32_t>(cl ? kMfWideSpan : kMfNarrowSpan, std::max<uint32_t>(1, (omax[cl] + 31) / 32));
+            m.lean = cl == 1 && kMfWideLean;
+            m.span = std::min<uint32_t>(cl ? kMfWideSpan : kMfNarrowSpan,
+                                        std::max<uint32_t>(1, (omax[cl] + 31) / 32));
             m.spans = (uint32_t)P.mspans.size();
             for (uint32_t k : mfk[cl])
                 for (uint32_t base = 0; base < P.slots[P.prod[k].out].words; base += 32 * m.span)
@@ -701,6 +704,7 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 mf.nitems = m.nspans, mf.span = m.span;
                 mf.vmax = m.vmax, mf.umax = m.umax;
                 mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span, mf.umax);
+                if (m.lean) mf.lean = 1, mf.wave_words = mul_mfma_lean_leaf_wave_words(mf.vmax, mf.span, mf.umax);
                 return launch_mul_mfma(mf, false, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
             };
             if (hm_status st = mf_launch(col.ppl, P->off_ppm, col.ppm); st) return st;

@@ -205,7 +205,9 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
 //    loads for much of its life; the host sizes the narrow spans so 16 waves' LDS slices fit.
 //  - leaves (LEAF true): no whole-U image either, only each group's window (mf_group_win), so a
 //    256-word leaf's LDS slice is ~9 KB instead of ~12.5 KB and 16 waves fit a CU.
-template <bool LEAF, bool LEAN = false>
+//  - wide schoolbook products (LEAF false, WIN true: U above kMfNarrowWords) the same way as the
+//    leaves: per-group U windows, spans of kMfWideLeanSpan tiles.
+template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN, LEAN ? HM_MFN_WPE : HM_MF_WPE)))
 mul_mfma_kernel(MulMfmaArgs P) {
@@ -247,7 +249,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
         for (int w = base + lane; w < wend; w += kWave) O[w] = 0u;
         return;
     }
-    constexpr bool WIN = LEAF && LEAN; // per-group U windows instead of the whole U image
+    static_assert(!WIN || LEAN, "windows come with the lean instance");
     uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
     const uint32_t rs_words = WIN ? mf_win_words(kMfG + 1) : mf_rs_words(P.umax);
     uint32_t *VI = RS + rs_words;
@@ -436,6 +438,8 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
     else if (leaf) hipLaunchKernelGGL(mul_mfma_kernel<true>, grid, block, lds, (hipStream_t)stream, a);
     else if (a.umax <= kMfNarrowWords)
         hipLaunchKernelGGL((mul_mfma_kernel<false, true>), grid, block, lds, (hipStream_t)stream, a);
+    else if (a.lean)
+        hipLaunchKernelGGL((mul_mfma_kernel<false, true, true>), grid, block, lds, (hipStream_t)stream, a);
     else hipLaunchKernelGGL(mul_mfma_kernel<false>, grid, block, lds, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
