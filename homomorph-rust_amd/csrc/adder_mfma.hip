@@ -35,6 +35,8 @@
 // bit 0 of its f32 encoding is the coefficient.  One v_alignbit per accumulator gathers them.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "mfma_gf2.h"
 
 namespace hm {
@@ -252,6 +254,7 @@ add_chain_mfma_kernel(AddArgs A) {
             const int n = max(nc, nab);
             for (int w = lane; w < n; w += kWave) C[w] = w < nab ? abi[w] : 0u;
             nc = nab;
+            degc = (int)rfl(rec[oD + 1]) - 1; // carry_{i+1} = ab_i
             tw = -1;
             wsync();
             stage_rec(i + 1);
@@ -300,6 +303,11 @@ add_chain_mfma_kernel(AddArgs A) {
         // the top tile's whole window: words 32(tiles-1) - D .. + 32 + 2 NC
         ring_fill<Cfg::kMirror>(C, ring, tab, 32 * (tiles - 1) - D, 32 + 2 * NC, lane);
         int ldeg = -1;
+        // deg(P_i * carry_i) = deg P_i + deg carry_i exactly (GF(2)[X] has no zero divisors), so
+        // when that is above deg ab_i it is carry_{i+1}'s degree; only otherwise (a short carry:
+        // ab_i may reach the top word) do the tiles track the highest set bit (wave-uniform)
+        const int alg = (int)rfl(rec[oD]) - 1 + degc;
+        const bool track = alg <= (int)rfl(rec[oD + 1]) - 1;
         // The accumulators start at 2^23 once per bit and keep accumulating tile after tile
         // (2^23 + every count stays below 2^24, exact): a tile's parities are bit 0 of its
         // accumulators XOR bit 0 before the tile.
@@ -316,6 +324,9 @@ add_chain_mfma_kernel(AddArgs A) {
         uint4 pf[kPrefetch];
 #pragma unroll
         for (int c = 0; c < kPrefetch; ++c) pf[c] = rbase(tiles - 1)[2 * c];
+        // the tile loop, instantiated with and without the degree tracking (TRACK: the branch is
+        // per bit, not per tile)
+        auto tile_loop = [&](auto TRACK) {
         for (int T = tiles - 1; T >= 0; --T) {
             wsync(); // ring images of this tile's window are written
             const uint4 *rb = rbase(T), *rbn = rbase(T - 1); // (T = 0: rbn reads are not used)
@@ -357,9 +368,16 @@ add_chain_mfma_kernel(AddArgs A) {
                 C[W] = v;
                 if (W >= wlo && W < capn) son[W] = v;
             }
-            if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
+            if constexpr (decltype(TRACK)::value)
+                if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
         }
-        const int deg = wave_max_i32(ldeg);
+        };
+        // (NC = 25: one instance, tracking always: a second copy of the loop costs spills in it
+        // at 168 VGPRs, and 5 VALU per tile weigh less against 25 MFMAs)
+        if constexpr (NC > 16) tile_loop(std::true_type{});
+        else if (track) tile_loop(std::true_type{});
+        else tile_loop(std::false_type{});
+        const int deg = (NC > 16 || track) ? wave_max_i32(ldeg) : alg;
         nc = deg >= 0 ? (deg >> 5) + 1 : 0;
         degc = deg;
         tw = 32 * tiles;
