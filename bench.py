@@ -608,9 +608,11 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     del c4a, c4b, o4, host
 
     # Multiplies (configs[3]) under an S(0) = 0 key, so that every product's decryption is
-    # checked: u8 multiply, batch 1024, and the low K result bits of the u32 circuit.
+    # checked: u8 multiply (batch 16384: the reference benches one value, so the batch is a
+    # throughput choice; 1024 values are one wave per SIMD), and the low K result bits of the u32
+    # circuit (configs[3]: batch 1024).
     mctx, mseed = s0_zero_context(device)
-    n8 = 1024
+    n8 = 16384
     a8 = np.random.default_rng(1).integers(0, 256, size=n8, dtype=np.uint8)
     b8 = np.random.default_rng(2).integers(0, 256, size=n8, dtype=np.uint8)
     ca, cbb = mctx.encrypt(a8), mctx.encrypt(b8)
@@ -636,7 +638,7 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
                      "roofline": mul_roofline(mctx, ca.bound, cbb.bound, 8, n8, ev_s / mreps,
                                               "u8 multiply"),
                      "cpu_baseline": cpu_m8}
-    # benches/u8.rs:31-37 "decipher after mul": decrypting the 1024 u8 products (the rem-heavy
+    # benches/u8.rs:31-37 "decipher after mul": decrypting the u8 products (the rem-heavy
     # case of the multiply's wide outputs), one HIP graph replay per step
     d8 = torch.empty((n8, 1), dtype=torch.uint8, device=device)
     coc = co._c()
