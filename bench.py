@@ -369,9 +369,10 @@ def s0_zero_context(device, params=PARAMS):
 
 def config0_lines(device, leg_s):
     """BASELINE.json configs[0]: the reference's `cargo bench --bench u8` plumbing (u8 encrypt,
-    decrypt and add at d = dp = tau = 64, delta = 1) -- on the GPU over a batch of 4096 u8 values,
-    each op one HIP graph replay per step, with the oracle's 1-thread rate of the same op beside
-    it."""
+    decrypt and add at d = dp = tau = 64, delta = 1) -- on the GPU over a batch of 65536 u8 values
+    (the reference benches one value: the batch is a throughput choice; 4096 left these
+    microsecond kernels launch-bound), each op one HIP graph replay per step, with the oracle's
+    1-thread rate of the same op beside it."""
     import ctypes
     from oracle import oracle_py as oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -382,7 +383,7 @@ def config0_lines(device, leg_s):
     c0.seed_rng(BENCH_SEED)
     c0.generate_secret_key()
     c0.generate_public_key()
-    n = 4096
+    n = 65536
     a_np = np.random.default_rng(31).integers(0, 256, size=n, dtype=np.uint8)
     b_np = np.random.default_rng(32).integers(0, 256, size=n, dtype=np.uint8)
     da = torch.from_numpy(a_np).to(device).reshape(n, 1)
