@@ -35,8 +35,6 @@
 // bit 0 of its f32 encoding is the coefficient.  One v_alignbit per accumulator gathers them.
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "mfma_gf2.h"
 
 namespace hm {
@@ -324,9 +322,6 @@ add_chain_mfma_kernel(AddArgs A) {
         uint4 pf[kPrefetch];
 #pragma unroll
         for (int c = 0; c < kPrefetch; ++c) pf[c] = rbase(tiles - 1)[2 * c];
-        // the tile loop, instantiated with and without the degree tracking (TRACK: the branch is
-        // per bit, not per tile)
-        auto tile_loop = [&](auto TRACK) {
         for (int T = tiles - 1; T >= 0; --T) {
             wsync(); // ring images of this tile's window are written
             const uint4 *rb = rbase(T), *rbn = rbase(T - 1); // (T = 0: rbn reads are not used)
@@ -368,16 +363,14 @@ add_chain_mfma_kernel(AddArgs A) {
                 C[W] = v;
                 if (W >= wlo && W < capn) son[W] = v;
             }
-            if constexpr (decltype(TRACK)::value)
+            // a wave-uniform branch (the empty volatile asm keeps the compiler from if-converting
+            // it into per-lane selects that run on every tile)
+            if (track) {
+                asm volatile("" ::: "memory");
                 if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
+            }
         }
-        };
-        // (NC = 25: one instance, tracking always: a second copy of the loop costs spills in it
-        // at 168 VGPRs, and 5 VALU per tile weigh less against 25 MFMAs)
-        if constexpr (NC > 16) tile_loop(std::true_type{});
-        else if (track) tile_loop(std::true_type{});
-        else tile_loop(std::false_type{});
-        const int deg = (NC > 16 || track) ? wave_max_i32(ldeg) : alg;
+        const int deg = track ? wave_max_i32(ldeg) : alg;
         nc = deg >= 0 ? (deg >> 5) + 1 : 0;
         degc = deg;
         tw = 32 * tiles;
