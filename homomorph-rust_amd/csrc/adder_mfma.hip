@@ -327,15 +327,22 @@ add_chain_mfma_kernel(AddArgs A) {
             const uint4 *rb = rbase(T), *rbn = rbase(T - 1); // (T = 0: rbn reads are not used)
             // the next tile's 32 new window words (old carry: below 32T; their ring slots are not
             // in this tile's window), one per lane pair, staged between this tile's MFMAs
+            // (tile 0 stages words -32-D+col too: its ring slots are outside tile 0's window, C
+            // reads below the halo stay inside the block's LDS, and the next bit refills its window
+            // before reading it, so no per-tile test is needed)
             const int fw = 32 * (T - 1) - D + col;
-            uint32_t fv = 0u;
-            uint2 fn = {0u, 0u};
-            // ab_i's word of this tile's output, read before the MFMAs (ab_i < 64 words: host plan)
+            uint32_t fv;
+            uint2 fn;
+            // ab_i's word of this tile's output, read before the MFMAs (ab_i < 64 words: host plan;
+            // a wave-uniform branch: tiles 0 and 1 at most)
             const int W = 32 * T + col;
-            const uint32_t abw = W < nab ? abi[W] : 0u;
+            uint32_t abw = 0u;
+            if (32 * T < nab) {
+                asm volatile("" ::: "memory");
+                abw = W < nab ? abi[W] : 0u;
+            }
             __builtin_amdgcn_s_setprio(1); // the MFMA phase keeps the pipe
             acc = tile_mfma<NC>(Af, rb, rbn, pf, acc, [&](int stage) {
-                if (T == 0) return;
                 // (the empty asm keep each stage's arithmetic from being hoisted into an earlier
                 // stage, where it would wait for the read of the stage before)
                 if (stage == 0) fv = C[fw];
