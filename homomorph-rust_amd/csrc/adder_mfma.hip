@@ -104,7 +104,7 @@ __device__ __forceinline__ void ring_put(uint32_t *ring, int w, int h, uint2 nb)
     const int s = w & (kMfmaRingSlots - 1);
     uint32_t *slot = &ring[s * 4 + 2 * h];
     *(uint2 *)slot = nb;
-    if (s < kMirror) *(uint2 *)(slot + 4 * kMfmaRingSlots) = nb;
+    if (kMirror >= kMfmaRingSlots || s < kMirror) *(uint2 *)(slot + 4 * kMfmaRingSlots) = nb;
 }
 
 // Nibble images of carry words [base, base + count) into the ring (count <= 64).  Lane l writes
@@ -361,20 +361,29 @@ add_chain_mfma_kernel(AddArgs A) {
             // XOR the bits of the accumulators before this tile
             const uint32_t tnow = acc_parities(acc);
             const uint32_t t = (tnow ^ gprev) << (4 * h);
+            // the two lane halves' bits meet by one v_permlane32_swap (VALU; no LDS round trip):
+            // lanes 0-31 keep their t in the first result and receive lanes 32-63's t in the
+            // second; only lanes 0-31 use the word (stores, degree), so the second operand is the
+            // dead previous gprev rather than a copy of t
+            const auto sw = __builtin_amdgcn_permlane32_swap(t, gprev, false, false);
             gprev = tnow;
-            // the two lane halves' bits meet by one v_permlane32_swap (VALU; no LDS round trip)
-            const auto sw = __builtin_amdgcn_permlane32_swap(t, t, false, false);
             const uint32_t word = sw[0] | sw[1];
             const uint32_t v = word ^ abw;
             if (h == 0) {
                 C[W] = v;
-                if (W >= wlo && W < capn) son[W] = v;
+                // (wave-uniform first: a tile wholly inside [wlo, capn) needs no per-lane test)
+                if (T >= 1 && 32 * T + 32 <= capn) {
+                    asm volatile("" ::: "memory");
+                    son[W] = v;
+                } else if (W >= wlo && W < capn) son[W] = v;
             }
             // a wave-uniform branch (the empty volatile asm keeps the compiler from if-converting
             // it into per-lane selects that run on every tile)
             if (track) {
                 asm volatile("" ::: "memory");
-                if (v) ldeg = max(ldeg, W * 32 + 31 - (int)__builtin_clz(v));
+                int Wq = W; // (opaque: its bit position is not strength-reduced into every tile)
+                asm volatile("" : "+v"(Wq));
+                if (h == 0 && v) ldeg = max(ldeg, Wq * 32 + 31 - (int)__builtin_clz(v));
             }
         }
         const int deg = track ? wave_max_i32(ldeg) : alg;
