@@ -322,9 +322,12 @@ add_chain_mfma_kernel(AddArgs A) {
         uint4 pf[kPrefetch];
 #pragma unroll
         for (int c = 0; c < kPrefetch; ++c) pf[c] = rbase(tiles - 1)[2 * c];
+        // (NC = 13: the window base carries over, this tile's is the previous tile's next)
+        const uint4 *rb = rbase(tiles - 1);
         for (int T = tiles - 1; T >= 0; --T) {
             wsync(); // ring images of this tile's window are written
-            const uint4 *rb = rbase(T), *rbn = rbase(T - 1); // (T = 0: rbn reads are not used)
+            if constexpr (NC > 16) rb = rbase(T); // (NC = 25: carried over, it spilled)
+            const uint4 *rbn = rbase(T - 1); // (T = 0: rbn reads are not used)
             // the next tile's 32 new window words (old carry: below 32T; their ring slots are not
             // in this tile's window), one per lane pair, staged between this tile's MFMAs
             // (tile 0 stages words -32-D+col too: its ring slots are outside tile 0's window, C
@@ -385,6 +388,7 @@ add_chain_mfma_kernel(AddArgs A) {
                 asm volatile("" : "+v"(Wq));
                 if (h == 0 && v) ldeg = max(ldeg, Wq * 32 + 31 - (int)__builtin_clz(v));
             }
+            rb = rbn;
         }
         const int deg = track ? wave_max_i32(ldeg) : alg;
         nc = deg >= 0 ? (deg >> 5) + 1 : 0;
