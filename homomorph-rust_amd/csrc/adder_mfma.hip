@@ -12,6 +12,8 @@
 //   bits e, so that
 //       out[32W + m] = sum_{c,h,e} A_c[m][(h,e)] * B_c[(h,e)][n]
 //       A_c[m][(h,e)] = P[32(D - 2c - h) + m - e]      (independent of the tile: built once per bit)
+//   (with the rows permuted, mfma_gf2.h row_bit: A row m computes output bit row_bit(m), so that
+//   each lane's 16 accumulators are one contiguous half of the output word)
 //       B_c[(h,e)][n] = C[32(32T + n - D + 2c + h) + e]
 //   with D = np (np = words of P_i: output word W takes carry words W-np .. W, since word q of P
 //   times word w of the carry reaches output words q+w and q+w+1) and NC = floor(np/2) + 1
@@ -279,7 +281,7 @@ add_chain_mfma_kernel(AddArgs A) {
         // j0 of chunk c = jb + 64c (jb >= 64 since D <= 2 NC - 1 < kRevWords - 2): one base word per
         // lane, chunk c at +8c words (immediate offsets), one shift for all chunks
         v8i Af[NC];
-        const int jb = 32 * (kRevWords - D + h) - 1 - col;
+        const int jb = 32 * (kRevWords - D + h) - 1 - row_bit(col); // (row-permuted tiles)
         const uint32_t *rw0 = RS + (jb >> 3);
         const uint32_t sh = 4u * (uint32_t)(jb & 7);
 #pragma unroll
@@ -359,11 +361,10 @@ add_chain_mfma_kernel(AddArgs A) {
                 }
             });
             __builtin_amdgcn_s_setprio(0);
-            // rows (j&3) + 8(j>>2) + 4h of column col: bit 0 of each accumulator, nibble q
-            // (accumulators 4q .. 4q+3) at bits 8q .. 8q+3 (rows 8q + 4h + i sit at bit 8q + 4h + i);
-            // XOR the bits of the accumulators before this tile
-            const uint32_t tnow = acc_parities(acc);
-            const uint32_t t = (tnow ^ gprev) << (4 * h);
+            // accumulator j of lane half h is output bit j + 16h (row-permuted tiles): its parity
+            // is bit 16 + j of tnow; XOR the bits of the accumulators before this tile
+            const uint32_t tnow = acc_parities_hi16(acc);
+            const uint32_t t = (tnow ^ gprev) >> (16 - 16 * h);
             // the two lane halves' bits meet by one v_permlane32_swap (VALU; no LDS round trip):
             // lanes 0-31 keep their t in the first result and receive lanes 32-63's t in the
             // second; only lanes 0-31 use the word (stores, degree), so the second operand is the

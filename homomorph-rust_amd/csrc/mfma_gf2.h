@@ -67,21 +67,21 @@ __device__ __forceinline__ v8i b_fragment(const uint4 &q) {
     return (v8i){(int)q.x, (int)q.y, (int)q.z, (int)q.w, 0, 0, 0, 0};
 }
 
-// The parities of one lane's 16 accumulators: rows (j&3) + 8(j>>2) + 4h of column col, as four
-// nibbles at bits 8q .. 8q+3 (q = j>>2) of the returned word (not yet shifted by 4h)
-__device__ __forceinline__ uint32_t acc_parities(const v16f &acc) {
-    uint32_t nq[4];
+// Row-permuted tiles (the adder's chain and the multiplier's products): A row m computes output bit row_bit(m) instead of bit m,
+// so that lane (col, h)'s accumulator j (D row (j&3) + 8(j>>2) + 4h) holds output bit j + 16h and
+// a lane's 16 parities are one contiguous half word: 15 funnel shifts gather them, with no
+// per-nibble shifts and ORs (round 4: 26 -> 20 VALU per tile; headline -0.4 %, configs[4]
+// -1.5 %, K = 16 -1.1 %).  The A fragments only read their operand from a permuted start.
+__host__ __device__ constexpr int row_bit(int m) { return (m & 3) + 4 * (m >> 3) + 16 * ((m >> 2) & 1); }
+// bit 16 + j = bit 0 of accumulator j (j = 0..15); bits 0..15 zero
+__device__ __forceinline__ uint32_t acc_parities_hi16(const v16f &acc) {
+    uint32_t x = __float_as_uint(acc[0]) << 31;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t x = 0u;
-#pragma unroll
-        for (int j = 4 * q; j < 4 * q + 4; ++j) x = funnel(__float_as_uint(acc[j]), x, 1);
-        nq[q] = x >> 28; // bit j-4q = accumulator j
-    }
-    return nq[0] | (nq[1] << 8) | (nq[2] << 16) | (nq[3] << 24);
+    for (int j = 1; j < 16; ++j) x = funnel(__float_as_uint(acc[j]), x, 1);
+    return x;
 }
 
-// Lane halves joined: lane (col, h) holds its half's rows shifted into place (t << 4h); one
+// Lane halves joined: lane (col, h) holds its half's bits in place (bits 16h .. 16h + 15); one
 // v_permlane32_swap brings the other half's, and both halves return output word col.
 __device__ __forceinline__ uint32_t join_halves(uint32_t t_shifted) {
     const auto sw = __builtin_amdgcn_permlane32_swap(t_shifted, t_shifted, false, false);

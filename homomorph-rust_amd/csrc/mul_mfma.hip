@@ -85,7 +85,8 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const uint32_t word = join_halves(acc_parities(acc[t]) << (4 * h));
+        // row-permuted tiles (mfma_gf2.h row_bit): accumulator j is output bit j + 16h
+        const uint32_t word = join_halves(acc_parities_hi16(acc[t]) >> (16 - 16 * h));
         if (h == 0) atomicXor(&OUT[32 * (T0 + t - Ts) + col], word); // this wave's slice only
     }
 }
@@ -94,7 +95,7 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
 template <int G>
 __device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int c0, v8i (&Af)[G]) {
     const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
-    const int jb = 32 * (R - D + h) - 1 - col;
+    const int jb = 32 * (R - D + h) - 1 - row_bit(col); // (row-permuted tiles)
     const uint32_t *rw0 = RS + (jb >> 3) + 8 * c0;
     const uint32_t sh = 4u * (uint32_t)(jb & 7);
 #pragma unroll
