@@ -48,6 +48,8 @@ MUL_LOW_BENCH = 16  # configs[3]: result bits of the u32 multiply that are run (
 BENCH_SEED = 0xB0B  # rank 0's keys and the mask stream (hm_ctx_seed_rng, the test contract)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP4_MFMA_PEAK_TFLOPS = 10000.0  # MI355X dense FP4 MFMA peak (MI355X_MICROARCH.md; not the sparse 20 PF)
+PCIE_PEAK_GBS = 63.0  # host link, PCIe Gen5 x16 one direction (MI355X_MICROARCH.md "Host link")
+MUL_BATCH = 1024  # configs[3]: "u32 homomorphic mul, batch=1024"
 
 
 def chain_bit_pairs(ba, bb):
@@ -601,17 +603,20 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     out["u32_add_pcie_inclusive"] = {
         "value": n4 * preps / wall, "unit": "adds/s", "batch": n4, "bytes_moved_per_step": moved,
         "note": "H2D inputs + add + D2H outputs per step",
-        "roofline": hbm_roofline(moved * preps, wall, "H2D + add + D2H (wall time of the step)",
-                                 "the bytes crossing PCIe per step over the step's wall time vs "
-                                 "the HBM peak (the step is PCIe-bound: these bytes cross the host "
-                                 "link, not only HBM)"),
+        "roofline": {"bound": "pcie", "achieved": moved * preps / wall / 1e9, "peak": PCIE_PEAK_GBS,
+                     "unit": "GB/s", "frac": moved * preps / wall / 1e9 / PCIE_PEAK_GBS,
+                     "kernel": "H2D copies + add + D2H copies (wall time of the step)",
+                     "note": "the bytes crossing the host link per step (inputs in, outputs and "
+                             "degrees out, one direction at a time on one stream) over the step's "
+                             "wall time vs PCIe Gen5 x16's 63 GB/s per direction"},
         "cpu_baseline": cpu_add if cpu_add is not None else {"value": None, "note": "--no-cpu"}}
     del c4a, c4b, o4, host
 
-    # Multiplies (configs[3]) under an S(0) = 0 key, so that every product's decryption is
-    # checked: u8 multiply (batch 16384: the reference benches one value, so the batch is a
+    # Multiplies under an S(0) = 0 key, so that every product's decryption is checked: the u8
+    # multiply (benches/u8.rs, batch n8 = 16384: the reference benches one value, so the batch is a
     # throughput choice; 1024 values are one wave per SIMD), and the low K result bits of the u32
-    # circuit (configs[3]: batch 1024).
+    # circuit at configs[3]'s own batch, MUL_BATCH = 1024 (plus a labelled batch-16384 aside at
+    # K = 16).
     mctx, mseed = s0_zero_context(device)
     n8 = 16384
     a8 = np.random.default_rng(1).integers(0, 256, size=n8, dtype=np.uint8)
@@ -668,8 +673,9 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     # carry-save circuit, bit-exact (tests: oracle fixture at K = 16, residue checks of the full
     # batch at K = 16 and of K = 20); the full u32 circuit is infeasible for any engine and is
     # priced, not run: the planner's own cost model (hm_mul_cost) scales the measured rate up
-    a32 = np.random.default_rng(3).integers(0, 2**32, size=n8, dtype=np.uint32)
-    b32 = np.random.default_rng(4).integers(0, 2**32, size=n8, dtype=np.uint32)
+    n32 = 16384  # encrypted values: configs[3]'s 1024 are the first MUL_BATCH of them
+    a32 = np.random.default_rng(3).integers(0, 2**32, size=n32, dtype=np.uint32)
+    b32 = np.random.default_rng(4).integers(0, 2**32, size=n32, dtype=np.uint32)
     c32a, c32b = mctx.encrypt(a32), mctx.encrypt(b32)
     # the oracle's K = 12 circuit on one value (the low 12 bits of u32 ciphertexts, as the engine
     # reads them); K >= 16 takes the oracle minutes to hours per value, so their CPU rates are this
@@ -694,13 +700,16 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
                 "extrapolated": True,
                 "sample": f"EXTRAPOLATED: the K = 12 oracle leg's {k12_pairs_s:.3g} word pairs/s "
                           f"(1 thread) applied to K = {k}'s {wp:.4g} word pairs (hm_mul_cost)"}
-    for k, nk in ((12, n8), (MUL_LOW_BENCH, n8), (20, 16)):
+    for name, k, nk in (("u32_mul_low12", 12, MUL_BATCH),
+                        (f"u32_mul_low{MUL_LOW_BENCH}", MUL_LOW_BENCH, MUL_BATCH),
+                        (f"u32_mul_low{MUL_LOW_BENCH}_batch{n32}", MUL_LOW_BENCH, n32),
+                        ("u32_mul_low20", 20, 16)):
         ob = H.mul_out_bounds(c32a.bound[:k], c32b.bound[:k])
         va, vb = H.value_slice(c32a, 0, nk), H.value_slice(c32b, 0, nk)
         cp = H.Ciphered.empty(nk, ob, device)
         H.mul_low_into(mctx, va, vb, k, cp)  # plan + workspace outside the timed loop
         mctx.synchronize()
-        reps = 1 if k >= 20 else 2 if k >= 16 else max(2, steps // 4)
+        reps = 1 if k >= 20 or nk > MUL_BATCH else 2 if k >= 16 else max(2, steps // 4)
         wall, ev_s = time_loop(lambda: H.mul_low_into(mctx, va, vb, k, cp), reps, 0, 1,
                                mctx.stream)
         mctx.synchronize()
@@ -710,16 +719,19 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
         want = (a32[:nk].astype(np.uint64) * b32[:nk]) & np.uint64((1 << k) - 1)
         cost = H.mul_cost(c32a.bound, c32b.bound, k)
         rate = nk * reps / wall
-        out[f"u32_mul_low{k}"] = {
+        out[name] = {
             "value": rate, "unit": f"u32 muls/s (result bits 0..{k - 1})", "batch": nk,
+            "config": "configs[3] (batch 1024)" if nk == MUL_BATCH else
+                      f"aside: configs[3]'s circuit at batch {nk} (not configs[3]'s batch)",
             "ms_per_batch": 1e3 * wall / reps, "kernel_ms_per_batch": 1e3 * ev_s / reps,
             "decrypt_correct": int(np.sum(lo == want)), "of": nk, "key_seed": mseed,
             "secret_key_s0": int(mctx.get_secret_key().limbs[0] & 1),
             "word_pairs_per_mul": cost["word_pairs"],
             "word_pairs_per_s": cost["word_pairs"] * rate,
-            "bit_exact": "tests/test_golden.py (K=16 oracle fixture, 8 values), "
-                         "test_gpu_properties.py (residue check of all 1024 K=16 products; "
-                         "K=20 Karatsuba = schoolbook + residue check), test_gpu_parity.py",
+            "bit_exact": "tests/test_golden.py (oracle fixtures: K=16, 8 values; K=20, 4 "
+                         "values), test_gpu_properties.py (residue check of all 1024 K=16 "
+                         "products; K=20 Karatsuba = schoolbook + residue check), "
+                         "test_gpu_parity.py",
             "roofline": mul_roofline(mctx, c32a.bound, c32b.bound, k, nk, ev_s / reps,
                                      f"u32 multiply, low {k} bits"),
             "cpu_baseline": cpu_mul_low(k)}

@@ -208,6 +208,19 @@ hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n) {
 
 } // namespace
 
+// The status an hm_* entry returns for the exception its function-try-block caught (HM_ABI_CATCH,
+// ctx.h): host containers throw std::bad_alloc; nothing is allowed to unwind into a C, Rust or
+// ctypes caller.
+hm_status hm::exception_status() noexcept {
+    try {
+        throw;
+    } catch (const std::bad_alloc &) {
+        return HM_ERR_OUT_OF_MEMORY;
+    } catch (...) {
+        return HM_ERR_INTERNAL;
+    }
+}
+
 // =============================================================================================
 extern "C" {
 
@@ -226,6 +239,8 @@ const char *hm_status_string(int s) { // int: any value a foreign caller passes 
     case HM_ERR_INVALID_CIPHERED_LENGTH: return "ciphered length is not a multiple of 8";
     case HM_ERR_BAD_INPUT: return "input degree does not match its limbs";
     case HM_ERR_RANDOMNESS: return "the OS random source failed";
+    case HM_ERR_OUT_OF_MEMORY: return "host memory allocation failed";
+    case HM_ERR_INTERNAL: return "internal error (C++ exception caught at the ABI)";
     }
     return "unknown status";
 }
@@ -233,12 +248,12 @@ const char *hm_status_string(int s) { // int: any value a foreign caller passes 
 uint32_t hm_abi_version(void) { return HM_ABI_VERSION; }
 
 hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, int device,
-                        hm_ctx **out) {
+                        hm_ctx **out) try {
     if (!out) return HM_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     if (d == 0 || dp == 0 || delta == 0 || tau == 0 || delta >= d) return HM_ERR_INVALID_PARAMETERS;
     hm_ctx *c = new (std::nothrow) hm_ctx();
-    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (!c) return HM_ERR_OUT_OF_MEMORY;
     c->d = d, c->dp = dp, c->delta = delta, c->tau = tau, c->device = device;
     uint64_t nonce0 = 0;
     if (!os_random(c->chacha_key, sizeof(c->chacha_key)) || !os_random(&nonce0, sizeof(nonce0))) {
@@ -269,11 +284,14 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
     hipDeviceProp_t prop{};
     c->fp4_mfma = hipGetDeviceProperties(&prop, device) == hipSuccess &&
                   std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    // test hook: HM_TEST_NO_FP4_MFMA=1 makes this context behave as on a device without the fp4
+    // MFMA, so the VALU fallbacks and the explicit-MFMA error path run on the gfx950 test box
+    if (const char *v = std::getenv("HM_TEST_NO_FP4_MFMA"); v && v[0] == '1') c->fp4_mfma = false;
     *out = c;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-void hm_ctx_destroy(hm_ctx *c) {
+void hm_ctx_destroy(hm_ctx *c) try {
     if (!c) return;
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
@@ -293,47 +311,48 @@ void hm_ctx_destroy(hm_ctx *c) {
     wipe(c->chacha_key, sizeof(c->chacha_key));
     wipe(&c->rng, sizeof(c->rng));
     delete c;
+} catch (...) {
 }
 
 uint64_t hm_ctx_generation(const hm_ctx *c) { return c ? c->generation : 0; }
 
-hm_status hm_ctx_trim(hm_ctx *c) {
+hm_status hm_ctx_trim(hm_ctx *c) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     HM_HIP(c, hipStreamSynchronize(c->stream));
     for (auto &r : c->retired) (void)hipFree(r.p);
     c->retired.clear();
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_stream(hm_ctx *c, void *s) {
+hm_status hm_ctx_set_stream(hm_ctx *c, void *s) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     c->stream = (hipStream_t)s; // NULL = the device's default (null) stream, as in HIP
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 void *hm_ctx_stream(const hm_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 hm_status hm_ctx_parameters(const hm_ctx *c, uint16_t *d, uint16_t *dp, uint16_t *delta,
-                            uint16_t *tau) {
+                            uint16_t *tau) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     if (d) *d = c->d;
     if (dp) *dp = c->dp;
     if (delta) *delta = c->delta;
     if (tau) *tau = c->tau;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_secret_key(hm_ctx *c, const uint64_t *limbs, size_t n) {
+hm_status hm_ctx_set_secret_key(hm_ctx *c, const uint64_t *limbs, size_t n) try {
     if (!c || !limbs || n == 0) return HM_ERR_INVALID_ARGUMENT; // from_bytes asserts non-empty
     drop_secret(c);
     c->sk.assign(limbs, limbs + n);
     c->has_sk = true;
     c->has_pk = false; // set_secret_key clears the public key (src/context.rs:568-571)
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_public_key(hm_ctx *c, const uint64_t *limbs, uint32_t tau, uint32_t lpp) {
+hm_status hm_ctx_set_public_key(hm_ctx *c, const uint64_t *limbs, uint32_t tau, uint32_t lpp) try {
     if (!c || !limbs || tau == 0 || lpp == 0) return HM_ERR_INVALID_ARGUMENT;
     c->pk.assign(limbs, limbs + (size_t)tau * lpp);
     c->pk_tau = tau, c->pk_cap = lpp;
@@ -343,9 +362,9 @@ hm_status hm_ctx_set_public_key(hm_ctx *c, const uint64_t *limbs, uint32_t tau, 
     hm_status st = upload_pk(c);
     if (st == HM_OK) c->has_pk = true;
     return st;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_seed_rng(hm_ctx *c, uint64_t seed) {
+hm_status hm_ctx_seed_rng(hm_ctx *c, uint64_t seed) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     // test contract: keys from SplitMix64(seed), masks from ChaCha20 keyed by SplitMix64(seed ^ K)
     c->seeded = true;
@@ -360,18 +379,18 @@ hm_status hm_ctx_seed_rng(hm_ctx *c, uint64_t seed) {
     HM_HIP(c, hipMemcpyAsync(c->d_nonce, &nonce0, sizeof(nonce0), hipMemcpyHostToDevice, c->stream));
     HM_HIP(c, hipStreamSynchronize(c->stream));
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_generate_secret_key(hm_ctx *c) { // src/context.rs:421-424
+hm_status hm_ctx_generate_secret_key(hm_ctx *c) try { // src/context.rs:421-424
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     std::vector<uint64_t> s;
     if (!random_poly(c, c->d, s)) return HM_ERR_RANDOMNESS;
     hm_status st = hm_ctx_set_secret_key(c, s.data(), s.size());
     wipe(s.data(), s.size() * 8);
     return st;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_generate_public_key(hm_ctx *c) { // src/context.rs:249-261, :444-454
+hm_status hm_ctx_generate_public_key(hm_ctx *c) try { // src/context.rs:249-261, :444-454
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
     // T_i = S*Q_i + X*R_i.  deg S is d for generated keys but any degree for a key set with
@@ -397,9 +416,9 @@ hm_status hm_ctx_generate_public_key(hm_ctx *c) { // src/context.rs:249-261, :44
     for (uint32_t i = 0; i < c->tau; ++i)
         for (size_t w = 0; w < cap && w < rows[i].size(); ++w) all[(size_t)i * cap + w] = rows[i][w];
     return hm_ctx_set_public_key(c, all.data(), c->tau, (uint32_t)cap);
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_get_secret_key(const hm_ctx *c, uint64_t *limbs, size_t cap, size_t *n) {
+hm_status hm_ctx_get_secret_key(const hm_ctx *c, uint64_t *limbs, size_t cap, size_t *n) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
     if (n) *n = c->sk.size();
@@ -408,10 +427,10 @@ hm_status hm_ctx_get_secret_key(const hm_ctx *c, uint64_t *limbs, size_t cap, si
         std::memcpy(limbs, c->sk.data(), c->sk.size() * 8);
     }
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, uint32_t *tau,
-                                uint32_t *lpp) {
+                                uint32_t *lpp) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     if (!c->has_pk) return HM_ERR_PUBLIC_KEY_UNSET;
     if (tau) *tau = c->pk_tau;
@@ -421,9 +440,9 @@ hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, ui
         std::memcpy(limbs, c->pk.data(), c->pk.size() * 8);
     }
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) {
+hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     if (enable && c->tev.empty()) {
@@ -441,9 +460,9 @@ hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) {
     c->time_chain = enable != 0;
     c->tev_used = 0;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) {
+hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) try {
     if (!c || !total_ms || !launches) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     HM_HIP(c, hipStreamSynchronize(c->stream));
@@ -456,41 +475,41 @@ hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) 
     *total_ms = t;
     *launches = (uint32_t)(c->tev_used / 2);
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_add_options(hm_ctx *c, uint32_t chain) {
+hm_status hm_ctx_set_add_options(hm_ctx *c, uint32_t chain) try {
     if (!c || chain > HM_ADD_CHAIN_VALU) return HM_ERR_INVALID_ARGUMENT;
     c->add_chain = chain;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) {
+hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) try {
     if (!c || (ka_min && (ka_leaf < 32 || ka_leaf > 512))) return HM_ERR_INVALID_ARGUMENT;
     c->ka_min = ka_min;
     c->ka_leaf = ka_leaf & ~31u;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_add_pipeline(hm_ctx *c, int enable) {
+hm_status hm_ctx_set_add_pipeline(hm_ctx *c, int enable) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     c->add_pipe = enable != 0;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_set_mul_products(hm_ctx *c, uint32_t products) {
+hm_status hm_ctx_set_mul_products(hm_ctx *c, uint32_t products) try {
     if (!c || products > HM_MUL_PRODUCTS_VALU) return HM_ERR_INVALID_ARGUMENT;
     if (products == HM_MUL_PRODUCTS_MFMA && !c->fp4_mfma) return HM_ERR_UNSUPPORTED;
     c->mul_products = products;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_validate_operation(const hm_ctx *c, hm_op op, uint16_t *req) {
+hm_status hm_validate_operation(const hm_ctx *c, hm_op op, uint16_t *req) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     const uint16_t m = min_d_over_delta(op);
     if (req) *req = m;
     if ((uint32_t)c->d < (uint32_t)m * (uint32_t)c->delta) return HM_ERR_INVALID_PARAMETERS;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 // A fresh ciphertext bit is a subset sum of public-key rows (plus the plaintext bit), so its
 // degree is at most max(d + dp, deg T_i): d + dp for generated keys, more for a loaded key.
@@ -509,7 +528,7 @@ uint64_t hm_batch_stride(uint32_t nbits, const uint32_t *bound) {
 }
 
 // Degree bounds of common.rs:37-56 (deg(xy) = deg x + deg y, deg(x+y) <= max).
-hm_status hm_add_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, uint32_t *out) {
+hm_status hm_add_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, uint32_t *out) try {
     if (!a || !b || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
     int64_t c = -1; // null carry
     for (uint32_t i = 0; i < L; ++i) {
@@ -524,23 +543,23 @@ hm_status hm_add_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, ui
         }
     }
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 } // extern "C"
 
 extern "C" {
 
 hm_status hm_mul_out_bounds(uint32_t L, const uint32_t *a, const uint32_t *b, int is_signed,
-                            uint32_t *out) {
+                            uint32_t *out) try {
     if (!a || !b || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
     std::vector<int64_t> res;
     if (!mul_result_bounds(L, L, a, b, is_signed != 0, res)) return HM_ERR_UNSUPPORTED;
     for (uint32_t i = 0; i < L; ++i) out[i] = (uint32_t)std::max<int64_t>(res[i], 0);
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 hm_status hm_mul_cost(uint32_t L, uint32_t k, const uint32_t *a, const uint32_t *b, int is_signed,
-                      double *word_pairs, double *out_bytes, double *max_degree) {
+                      double *word_pairs, double *out_bytes, double *max_degree) try {
     if (!a || !b || L == 0 || L > HM_MAX_BITS || k == 0 || k > L) return HM_ERR_INVALID_ARGUMENT;
     (void)is_signed; // the signed corners (+1 in column L-1) change no bound
     double w, o, m;
@@ -549,17 +568,17 @@ hm_status hm_mul_cost(uint32_t L, uint32_t k, const uint32_t *a, const uint32_t 
     if (out_bytes) *out_bytes = o;
     if (max_degree) *max_degree = m;
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 hm_status hm_mul_plan_work(hm_ctx *c, uint32_t L, uint32_t k, const uint32_t *a, const uint32_t *b,
-                          int is_signed, double *word_pairs) {
+                          int is_signed, double *word_pairs) try {
     if (!c || !a || !b || !word_pairs || L == 0 || L > HM_MAX_BITS || k == 0 || k > L)
         return HM_ERR_INVALID_ARGUMENT;
     return mul_plan_work(c, L, k, a, b, is_signed != 0 && k == L, *word_pairs);
-}
+} HM_ABI_CATCH
 
 hm_status hm_gate_out_bounds(hm_op g, uint32_t L, const uint32_t *a, const uint32_t *b,
-                             uint32_t *out) {
+                             uint32_t *out) try {
     if (!a || !out || L == 0 || L > HM_MAX_BITS) return HM_ERR_INVALID_ARGUMENT;
     if (g != HM_OP_NOT && !b) return HM_ERR_INVALID_ARGUMENT;
     for (uint32_t i = 0; i < L; ++i) {
@@ -574,11 +593,11 @@ hm_status hm_gate_out_bounds(hm_op g, uint32_t L, const uint32_t *a, const uint3
         out[i] = (uint32_t)v;
     }
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 // ------------------------------------------------------------------ cipher
 hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, const uint8_t *masks,
-                           hm_batch *out) {
+                           hm_batch *out) try {
     if (!c || !out) return HM_ERR_INVALID_ARGUMENT;
     if (!c->has_pk) return HM_ERR_PUBLIC_KEY_UNSET;
     if (hm_status st = check_batch(out); st) return st;
@@ -618,15 +637,15 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     int r = launch_encrypt(E, c->stream);
     if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_random_bytes(hm_ctx *c, uint8_t *dst, size_t nbytes) {
+hm_status hm_random_bytes(hm_ctx *c, uint8_t *dst, size_t nbytes) try {
     if (!c || (nbytes && !dst)) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     return draw_random(c, dst, nbytes);
-}
+} HM_ABI_CATCH
 
-hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) {
+hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) try {
     if (!c || !in) return HM_ERR_INVALID_ARGUMENT;
     if (!c->has_sk) return HM_ERR_SECRET_KEY_UNSET;
     if (in->nbits % 8) return HM_ERR_INVALID_CIPHERED_LENGTH; // cipher.rs:218-220
@@ -653,10 +672,10 @@ hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) {
         if (cap_of(in->bound[i]) != D.ucap) D.ucap = 0;
     DeviceGuard g(c->device);
     return launch_decrypt(D, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
 // ------------------------------------------------------------------ operations
-hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch *out) {
+hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch *out) try {
     if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
     if (hm_status st = hm_validate_operation(c, HM_OP_ADD, nullptr); st) return st;
     for (const hm_batch *x : {a, b, (const hm_batch *)out})
@@ -802,10 +821,10 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         return HM_OK;
     }
     return launch_add(A, c->stream, ev[0], ev[1]) ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
 hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,
-                       hm_batch *out) {
+                       hm_batch *out) try {
     if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
     if (hm_status st = hm_validate_operation(c, is_signed ? HM_OP_MUL_SIGNED : HM_OP_MUL, nullptr); st)
         return st;
@@ -814,10 +833,10 @@ hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_s
     if (a->nbits != b->nbits || a->nbits != out->nbits || a->n != b->n || a->n != out->n)
         return HM_ERR_INVALID_ARGUMENT;
     return mul_columns(c, a, b, a->nbits, is_signed != 0, out);
-}
+} HM_ABI_CATCH
 
 hm_status hm_mul_low_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t k,
-                           hm_batch *out) {
+                           hm_batch *out) try {
     if (!c || !a || !b || !out) return HM_ERR_INVALID_ARGUMENT;
     if (hm_status st = hm_validate_operation(c, HM_OP_MUL, nullptr); st) return st;
     for (const hm_batch *x : {a, b, (const hm_batch *)out})
@@ -826,10 +845,10 @@ hm_status hm_mul_low_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint
         a->n != out->n)
         return HM_ERR_INVALID_ARGUMENT;
     return mul_columns(c, a, b, k, false, out);
-}
+} HM_ABI_CATCH
 
 hm_status hm_gate_batch(hm_ctx *c, hm_op gate, const hm_batch *a, const hm_batch *b,
-                        hm_batch *out) {
+                        hm_batch *out) try {
     if (!c || !a || !out) return HM_ERR_INVALID_ARGUMENT;
     if (gate > HM_OP_NOT) return HM_ERR_INVALID_ARGUMENT;
     if (hm_status st = hm_validate_operation(c, gate, nullptr); st) return st;
@@ -869,7 +888,7 @@ hm_status hm_gate_batch(hm_ctx *c, hm_op gate, const hm_batch *a, const hm_batch
     fill_bounds(G.ob, out);
     DeviceGuard g(c->device);
     return launch_gate(G, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
 // ------------------------------------------------------------------ polynomial primitives
 static PolyArgs poly_args(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) {
@@ -882,22 +901,22 @@ static PolyArgs poly_args(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_po
     return P;
 }
 
-hm_status hm_poly_add_batch(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) {
+hm_status hm_poly_add_batch(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) try {
     if (!c || !a || !b || !out || a->n != b->n || a->n != out->n) return HM_ERR_INVALID_ARGUMENT;
     if (!a->cap || !b->cap || out->cap < std::max(a->cap, b->cap)) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     return launch_poly_add(poly_args(c, a, b, out), c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_poly_mul_batch(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) {
+hm_status hm_poly_mul_batch(hm_ctx *c, const hm_polys *a, const hm_polys *b, hm_polys *out) try {
     if (!c || !a || !b || !out || a->n != b->n || a->n != out->n) return HM_ERR_INVALID_ARGUMENT;
     if (!a->cap || !b->cap || out->cap < a->cap + b->cap) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     return launch_poly_mul(poly_args(c, a, b, out), c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
 hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, size_t sn,
-                            hm_polys *out) {
+                            hm_polys *out) try {
     if (!c || !a || !out || !s || sn == 0 || a->n != out->n) return HM_ERR_INVALID_ARGUMENT;
     if (!a->cap || out->cap < a->cap) return HM_ERR_INVALID_ARGUMENT;
     bool nz = false;
@@ -914,7 +933,14 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
         // l0 = deg S / 64 on; size and build time are bounded by the dividend's capacity whatever
         // the divisor's degree (a divisor above every dividend needs no table: zt = null).
         const size_t l0 = ds / 64, tcols = acap - l0, sl = ds / 64 + 1;
-        if ((double)ds * tcols * 8 > 4.0 * (1ull << 30)) return HM_ERR_UNSUPPORTED; // host memory
+        if ((double)ds * tcols * 8 > 1.0 * (1ull << 30)) return HM_ERR_UNSUPPORTED; // host memory
+        const bool cached = c->d_s && c->rem_acap == acap && c->rem_gen == c->generation &&
+                            c->rem_key.size() == sl && std::equal(s, s + sl, c->rem_key.begin());
+        if (cached) {
+            T = RemTable{c->d_s, (uint32_t)ds, (uint32_t)l0, (uint32_t)tcols};
+            const int rc = launch_poly_rem(poly_args(c, a, nullptr, out), T, c->stream);
+            return rc ? hip_fail(c, hipGetLastError()) : HM_OK;
+        }
         std::vector<uint64_t> zt(ds * tcols, 0);
         // X^k mod S for the 64 k of column limb l0 + t: unit bits below deg S, then r = X * r mod
         // S; each block of 64 vectors is transposed word by word into the rows
@@ -958,12 +984,13 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
         HM_HIP(c, hipMemcpyAsync(c->d_s, zt.data(), zt.size() * 8, hipMemcpyHostToDevice, c->stream));
         HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer is released after return
         T = RemTable{c->d_s, (uint32_t)ds, (uint32_t)l0, (uint32_t)tcols};
+        c->rem_key.assign(s, s + sl), c->rem_acap = acap, c->rem_gen = c->generation;
     }
     const int rc = launch_poly_rem(poly_args(c, a, nullptr, out), T, c->stream);
     return rc ? hip_fail(c, hipGetLastError()) : HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_ctx_synchronize(hm_ctx *c) {
+hm_status hm_ctx_synchronize(hm_ctx *c) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
     HM_HIP(c, hipStreamSynchronize(c->stream));
@@ -975,6 +1002,6 @@ hm_status hm_ctx_synchronize(hm_ctx *c) {
         return HM_ERR_HIP;
     }
     return (hm_status)st;
-}
+} HM_ABI_CATCH
 
 } // extern "C"

@@ -39,6 +39,11 @@ struct hm_ctx {
     uint32_t z_limbs = 0;
     uint64_t *d_s = nullptr;           // divisor scratch for hm_poly_rem_batch
     size_t d_s_limbs = 0;
+    // hm_poly_rem_batch's remainder table in d_s is cached for (divisor, dividend capacity):
+    // a repeated divisor skips the host build and the upload
+    std::vector<uint64_t> rem_key;
+    size_t rem_acap = 0;
+    uint64_t rem_gen = 0;
     uint32_t *d_ws_add = nullptr;      // adder workspace (validated inputs, per-bit a_i*b_i)
     size_t ws_add_bytes = 0;
     uint32_t *d_mws = nullptr;         // column multiplier arena (mul_columns)
@@ -133,6 +138,15 @@ inline hm_status hip_fail(hm_ctx *c, hipError_t e) {
     if (c) c->last_hip = e;
     return HM_ERR_HIP;
 }
+
+// Every hm_* entry returning hm_status is a function-try-block ending in HM_ABI_CATCH, so no C++
+// exception (std::bad_alloc from a host container above all) crosses the C ABI
+// (include/homomorph_gpu.h: HM_ERR_OUT_OF_MEMORY, HM_ERR_INTERNAL).
+hm_status exception_status() noexcept;
+#define HM_ABI_CATCH                                                                              \
+    catch (...) {                                                                                 \
+        return hm::exception_status();                                                            \
+    }
 
 #define HM_HIP(ctx, expr)                                                                         \
     do {                                                                                          \

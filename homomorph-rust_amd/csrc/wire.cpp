@@ -66,7 +66,7 @@ uint64_t hm_wire_bytes(uint32_t nbits, const uint32_t *bound, uint64_t n) {
 }
 
 hm_status hm_wire_peek(const uint8_t *src, size_t len, uint32_t *nbits, uint64_t *n,
-                       uint32_t *bound) {
+                       uint32_t *bound) try {
     if (!src || len < kHeader) return HM_ERR_INVALID_ARGUMENT;
     if (std::memcmp(src, kMagic, 4) || rd32(src + 4) != kVersion || rd32(src + 12) != 0)
         return HM_ERR_INVALID_ARGUMENT;
@@ -81,9 +81,9 @@ hm_status hm_wire_peek(const uint8_t *src, size_t len, uint32_t *nbits, uint64_t
     if (n) *n = nv;
     if (bound) std::memcpy(bound, bd, 4ull * nb);
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_wire_encode(hm_ctx *c, const hm_batch *in, uint8_t *dst, size_t cap) {
+hm_status hm_wire_encode(hm_ctx *c, const hm_batch *in, uint8_t *dst, size_t cap) try {
     if (!c || !dst) return HM_ERR_INVALID_ARGUMENT;
     if (hm_status st = hm::check_batch(in); st) return st;
     Layout L;
@@ -102,9 +102,9 @@ hm_status hm_wire_encode(hm_ctx *c, const hm_batch *in, uint8_t *dst, size_t cap
     HM_HIP(c, hipMemcpy(dst + L.limb_off, in->limbs, 8ull * in->n * L.stride,
                         hipMemcpyDeviceToHost));
     return HM_OK;
-}
+} HM_ABI_CATCH
 
-hm_status hm_wire_decode(hm_ctx *c, const uint8_t *src, size_t len, hm_batch *out) {
+hm_status hm_wire_decode(hm_ctx *c, const uint8_t *src, size_t len, hm_batch *out) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     if (hm_status st = hm::check_batch(out); st) return st;
     uint32_t nb = 0;
@@ -132,6 +132,6 @@ hm_status hm_wire_decode(hm_ctx *c, const uint8_t *src, size_t len, hm_batch *ou
     HM_HIP(c, hipMemcpy(out->limbs, src + L.limb_off, 8ull * nv * L.stride,
                         hipMemcpyHostToDevice));
     return HM_OK;
-}
+} HM_ABI_CATCH
 
 } // extern "C"

@@ -72,6 +72,8 @@ def _check(st: int, what: str):
         raise CipherError(st, what)
     if st == _lib.ERR_DIVIDE_BY_ZERO:
         raise ZeroDivisionError("attempt to divide by zero")  # polynomial.rs:319-322
+    if st == _lib.ERR_OUT_OF_MEMORY:
+        raise MemoryError(f"{what}: {_lib.status_string(st)}")
     raise EngineError(st, what)
 
 

@@ -28,6 +28,8 @@ ERR_INVALID_ARGUMENT = 9
 ERR_INVALID_CIPHERED_LENGTH = 10
 ERR_BAD_INPUT = 11
 ERR_RANDOMNESS = 12
+ERR_OUT_OF_MEMORY = 13
+ERR_INTERNAL = 14
 
 # hm_op
 OP_AND, OP_OR, OP_XOR, OP_NOT, OP_ADD, OP_MUL, OP_MUL_SIGNED = range(7)

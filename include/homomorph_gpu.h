@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 2
+#define HM_ABI_VERSION 3
 #define HM_MAX_BITS 128 /* u128 is the widest type with impls (src/impls/numbers/uint.rs:58) */
 
 typedef enum hm_status {
@@ -60,6 +60,10 @@ typedef enum hm_status {
     HM_ERR_BAD_INPUT = 11,
     /* CipherError::Randomness (src/cipher.rs:18-24): the OS random source failed */
     HM_ERR_RANDOMNESS = 12,
+    /* a host-side allocation failed (std::bad_alloc inside the library, caught at the entry) */
+    HM_ERR_OUT_OF_MEMORY = 13,
+    /* any other C++ exception raised inside the library, caught at the entry */
+    HM_ERR_INTERNAL = 14,
 } hm_status;
 
 /* Operation marker types and their OperationRequirement::MIN_D_OVER_DELTA
@@ -224,8 +228,10 @@ hm_status hm_mul_cost(uint32_t nbits, uint32_t k, const uint32_t *a_bound, const
 /* The same carry products as the context's plan for hm_mul_low_batch / hm_mul_batch (k = nbits)
  * runs them, with the context's strategy options (hm_ctx_set_mul_options, _products): a schoolbook
  * product counts its word pairs at the static bounds (as hm_mul_cost does), a Karatsuba product its
- * leaf products' word pairs.  No device work runs; the plan is built and cached (its task tables
- * uploaded) as the multiply would; HM_ERR_UNSUPPORTED beyond the engine's limits.  The bench's
+ * leaf products' word pairs.  No kernel runs, but the plan is built and cached as the multiply
+ * would: its task tables are allocated in device memory and copied (synchronously) on the
+ * context's stream, so this call is not free and must not be made while that stream is being
+ * captured into a graph; HM_ERR_UNSUPPORTED beyond the engine's limits.  The bench's
  * multiply rooflines use it as the issued work. */
 hm_status hm_mul_plan_work(hm_ctx *ctx, uint32_t nbits, uint32_t k, const uint32_t *a_bound,
                            const uint32_t *b_bound, int is_signed, double *word_pairs);

@@ -45,6 +45,9 @@ CASES = {
     # SURVEY §8(d) configs[3] / row A14: the low 16 result bits of the u32 multiply (the circuit's
     # columns 0..15), stored as degrees + a SHA-256 per value (the outputs are ~200 KB a value)
     "mullow16_u32_d128": ("mullow16", (128, 128, 1, 128), np.uint32, 8, 111),
+    # result bits 16..19 too (columns 0..19): ~30 CPU-minutes per value on the oracle, one value
+    # per OpenMP thread; test_golden regenerates it only with HM_SLOW_GOLDEN=1
+    "mullow20_u32_d128": ("mullow20", (128, 128, 1, 128), np.uint32, 4, 112),
 }
 
 

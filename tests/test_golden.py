@@ -47,6 +47,10 @@ def test_oracle_reproduces_golden(oracle, name):
     op, ob = str(g["op"]), g["out_bound"]
     if op.startswith("mullow"):  # low k bits of the u32 multiply: degrees + per-value SHA-256
         k = int(g["k"])
+        if k >= 20 and os.environ.get("HM_SLOW_GOLDEN") != "1":
+            # ~30 CPU-minutes per value: the inputs were re-checked above; the product is
+            # regenerated only on request (make_golden.py made it with this oracle)
+            pytest.skip("K >= 20 oracle regeneration takes ~30 min per value (HM_SLOW_GOLDEN=1)")
         l1, d1, b1 = low_bits(la, da, bound, n, k)
         l2, d2, b2 = low_bits(lb, db, bound, n, k)
         oracle.set_threads(n)

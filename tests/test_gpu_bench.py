@@ -39,12 +39,13 @@ def test_bench_every_line_has_roofline_and_cpu_baseline():
     assert "error" not in sec, sec.get("error")
     for name in ("u32_encrypt_decrypt", "u32_encrypt", "u32_decrypt_fresh", "u32_decrypt_after_add",
                  "u32_add_pcie_inclusive", "u8_mul", "u8_decrypt_after_mul", "u32_mul_low12",
-                 "u32_mul_low16", "u32_mul_low20", "u32_mul_full_extrapolated", "mixed_config4",
+                 "u32_mul_low16", "u32_mul_low16_batch16384", "u32_mul_low20", "u32_mul_full_extrapolated", "mixed_config4",
                  "config0_u8_encrypt", "config0_u8_decrypt", "config0_u8_add"):
         line = sec[name]
         assert line["value"] > 0, name
         r = line["roofline"]
-        assert r["bound"] in ("hbm", "mfma") and r["peak"] > 0 and r["achieved"] > 0, name
+        assert r["bound"] in ("hbm", "mfma", "pcie") and r["peak"] > 0 and r["achieved"] > 0, name
+        assert (r["bound"] == "pcie") == (name == "u32_add_pcie_inclusive"), name
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9, name
         assert r["frac"] <= 1.0, (name, r["frac"])  # issued work, never an algorithm's count
         c = line["cpu_baseline"]
@@ -53,6 +54,9 @@ def test_bench_every_line_has_roofline_and_cpu_baseline():
     assert sec["config0_u8_decrypt"]["verified"]
     assert sec["config0_u8_add"]["verified"]["correct_sums"] == sec["config0_u8_add"]["batch"]
     assert sec["u32_mul_low16"]["cpu_baseline"]["extrapolated"] is True
+    # configs[3] names batch 1024; the batch-16384 rate is a labelled aside
+    assert sec["u32_mul_low12"]["batch"] == sec["u32_mul_low16"]["batch"] == 1024
+    assert sec["u32_mul_low16_batch16384"]["batch"] == 16384
     assert sec["u32_mul_low12"]["cpu_baseline"].get("extrapolated") is None
     m = sec["mixed_config4"]
     assert m["verified"]["correct_sums"] == m["verified"]["correct_products"] == m["global_batch"]

@@ -96,6 +96,26 @@ def test_poly_rem(H, oracle, cap, sdeg):
         assert np.array_equal(rl[i, : len(ref)], ref) and not rl[i, len(ref):].any()
 
 
+def test_poly_rem_table_cache(H, oracle):
+    """The remainder table is cached per (divisor, dividend capacity): a second call with the same
+    divisor reuses it, and a different divisor of the same length or a wider dividend rebuilds it."""
+    rng = np.random.default_rng(404)
+    ctx = make_ctx(H, (64, 64, 1, 64), 2)
+    S1 = _rand_polys(rng, 1, 3, maxdeg=150)[0]
+    S1[150 // 64] |= np.uint64(1 << (150 % 64))
+    S2 = S1.copy()
+    S2[0] ^= np.uint64(0b1010)
+    for S, cap in ((S1, 9), (S1, 9), (S2, 9), (S2, 30), (S1, 9)):
+        A = _rand_polys(rng, 32, cap)
+        pr = ctx.poly_rem(H.Polys.from_host(A, ctx.device), S)
+        ctx.synchronize()
+        rl, rd = pr.to_host()
+        for i in range(len(A)):
+            ref, rdeg = oracle.poly_rem(A[i], S)
+            assert rd[i] == rdeg
+            assert np.array_equal(rl[i, : len(ref)], ref) and not rl[i, len(ref):].any()
+
+
 def test_poly_rem_errors(H):
     ctx = make_ctx(H, (64, 64, 1, 64), 3)
     p = H.Polys.from_host(np.ones((2, 2), dtype=np.uint64), ctx.device)
@@ -300,6 +320,45 @@ def test_add_chain_mfma_unsupported(H):
     with pytest.raises(H.EngineError):
         ctx.apply2(H.HomomorphicAddition, a, a)
         ctx.synchronize()
+
+
+def test_no_fp4_mfma_fallback(H, oracle, monkeypatch):
+    """A context on a device without the gfx950 fp4 MFMA (forced with the HM_TEST_NO_FP4_MFMA=1
+    hook, read at context creation): the AUTO strategies take the VALU carry chain and the VALU
+    products, bit-exact against the oracle, and an explicit MFMA request is HM_ERR_UNSUPPORTED
+    (the products at the setter, the chain at the add)."""
+    from homomorph import _lib
+    monkeypatch.setenv("HM_TEST_NO_FP4_MFMA", "1")
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 61)
+    monkeypatch.delenv("HM_TEST_NO_FP4_MFMA")
+    sk, pk, _ = keys(*params, 61)
+    with pytest.raises(H.EngineError) as e:
+        ctx.set_mul_products("mfma")
+    assert e.value.status == _lib.ERR_UNSUPPORTED
+    n = 4
+    a, b, ma, mb, ca, cb = _pair(H, ctx, params, np.uint8, n, 62)
+    bound = fresh_bound(128, 128, 8)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a), ma, bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b), mb, bound)
+    cs = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    cp = ctx.apply2(H.HomomorphicMultiplication, ca, cb)
+    ctx.synchronize()
+    ob = H.add_out_bounds(bound, bound)
+    rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, 8, n, ob)
+    assert_batches_equal(*cs.to_host(), rl, rd, ob, n, "VALU-fallback add")
+    ob = H.mul_out_bounds(bound, bound)
+    rl, rd = oracle.mul_batch(la, da, bound, lb, db, bound, 8, n, ob)
+    assert_batches_equal(*cp.to_host(), rl, rd, ob, n, "VALU-fallback mul")
+    assert np.array_equal(ctx.decrypt(cs), (a.astype(int) + b).astype(np.uint8))
+    ctx.set_add_options("mfma")
+    with pytest.raises(H.EngineError) as e:
+        ctx.apply2(H.HomomorphicAddition, ca, cb)
+        ctx.synchronize()
+    assert e.value.status == _lib.ERR_UNSUPPORTED
+    # a context created without the hook on the same device uses the matrix cores again
+    ctx2 = make_ctx(H, params, 61)
+    ctx2.set_mul_products("mfma")
 
 
 def test_successive_add(H, oracle):

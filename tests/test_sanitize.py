@@ -5,7 +5,10 @@ engine library's host code, run on the CPU (GPU sanitizers are not available on 
   gates -> decrypt round trip through oracle/homomorph_oracle.c;
 - tests/sanitize/capi_san.cpp: every host-only C-ABI entry point (status strings, bounds, the
   multiplier cost model, strides, the wire-format parser under 20k corrupted headers, NULL
-  contexts), with the device kernels linked in unsanitised.
+  contexts), with the device kernels linked in unsanitised;
+- tests/sanitize/capi_oom.cpp (not sanitised): every allocation inside the multiplier's plan
+  builder failed in turn, each call returning HM_ERR_OUT_OF_MEMORY instead of throwing across
+  the C ABI.
 Any sanitizer report aborts the binary (-fno-sanitize-recover=all) and fails the test.
 """
 import os
@@ -42,3 +45,8 @@ def test_oracle_under_asan_ubsan(built):
 
 def test_engine_host_code_under_asan_ubsan(built):
     assert "ok" in _run(os.path.join(built, "capi_san"))
+
+
+def test_engine_abi_returns_oom_instead_of_throwing(built):
+    out = _run(os.path.join(built, "capi_oom"))
+    assert "ok" in out and "allocation points" in out
