@@ -607,16 +607,6 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
         if (out->bound[i] < c->pk_maxdeg) return HM_ERR_INVALID_ARGUMENT;
     if (out->n == 0) return HM_OK;
     DeviceGuard g(c->device);
-    if (!masks) {
-        // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): here the
-        // device ChaCha20 stream, drawn into the context's mask buffer right before the launch
-        const size_t mb = (size_t)out->n * out->nbits * ((c->pk_tau + 7) / 8);
-        const size_t need = (mb + 63) & ~(size_t)63;
-        if (need > c->masks_bytes && c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
-        HM_HIP(c, grow(c, c->d_masks, c->masks_bytes, need));
-        if (hm_status st = draw_random(c, c->d_masks, mb); st) return st;
-        masks = c->d_masks;
-    }
     EncArgs E{};
     E.pk = c->d_pk, E.tau = c->pk_tau, E.pk_cap = c->pk_cap;
     E.pk_tab = c->d_pk_tab;
@@ -624,7 +614,7 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     E.lognbits = -1;
     for (int s = 0; s < 8; ++s)
         if ((8u * nbytes) == (1u << s)) E.lognbits = s;
-    E.data = data, E.nbytes = nbytes, E.masks = masks;
+    E.data = data, E.nbytes = nbytes;
     E.out = batch_arg(out);
     E.n = out->n;
     E.status = c->d_status;
@@ -634,7 +624,29 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
         E.ooff.b[i] = o, o += cap_of(out->bound[i]);
         E.uniform_cap &= cap_of(out->bound[i]) == c->pk_cap;
     }
-    int r = launch_encrypt(E, c->stream);
+    if (!masks && encrypt_fusable(E)) {
+        // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): the device
+        // ChaCha20 stream, drawn inside the encryption kernel (the same keystream bytes a draw into
+        // the mask buffer would hold, so the masks never round-trip HBM)
+        RandArgs R{};
+        std::memcpy(R.key, c->chacha_key, sizeof(R.key));
+        R.nonce = c->d_nonce;
+        const int r = launch_encrypt(E, &R, c->stream);
+        wipe(R.key, sizeof(R.key));
+        if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
+        return r ? hip_fail(c, hipGetLastError()) : HM_OK;
+    }
+    if (!masks) {
+        // otherwise the stream is drawn into the context's mask buffer right before the launch
+        const size_t mb = (size_t)out->n * out->nbits * ((c->pk_tau + 7) / 8);
+        const size_t need = (mb + 63) & ~(size_t)63;
+        if (need > c->masks_bytes && c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
+        HM_HIP(c, grow(c, c->d_masks, c->masks_bytes, need));
+        if (hm_status st = draw_random(c, c->d_masks, mb); st) return st;
+        masks = c->d_masks;
+    }
+    E.masks = masks;
+    int r = launch_encrypt(E, nullptr, c->stream);
     if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
 } HM_ABI_CATCH

@@ -109,22 +109,105 @@ __device__ __forceinline__ void enc_lookup2(uint32_t *acc, const uint4 *tab4, ui
     }
 }
 
+#ifndef HM_ENC_NT
+#define HM_ENC_NT 0 // non-temporal ciphertext stores (A/B knob)
+#endif
+// The wave's 64 ciphertext bits t0 .. t0 + 63 once their subset sums are in acc: the plaintext
+// bit, the degree, and the stores (uniform caps: the wave's 64 * PC consecutive output limbs,
+// transposed through its LDS stage and stored coalesced; otherwise per bit at its offset)
+template <int PC>
+__device__ __forceinline__ void enc_finish(const EncArgs &E, uint64_t *acc, uint64_t *st,
+                                           uint64_t t0, uint64_t total, bool live, uint64_t e,
+                                           uint32_t k, uint32_t nbits) {
+    const uint32_t lane = threadIdx.x & 63u;
+    // mask bits at or above tau select nothing: the table rows past tau are zero, and the
+    // reference reads exactly ceil(tau/8) bytes, bits >= tau unused (cipher.rs:105-110)
+    acc[0] ^= (E.data[e * E.nbytes + k / 8] >> (k % 8)) & 1u; // add_bool_assign (:112)
+    int deg = 0;
+#pragma unroll
+    for (int l = 0; l < PC; ++l)
+        if (acc[l]) deg = l * 64 + 63 - __builtin_clzll(acc[l]);
+    if (live) {
+        if ((uint32_t)deg > E.ob.b[k]) flag(E.status, HM_ERR_CAPACITY);
+        E.out.degree[e * nbits + k] = (uint32_t)deg;
+    }
+    if (E.uniform_cap) {
+        // limb l of bit t at t*PC + l: lane j writes limb j, j + 64, ...
+#pragma unroll
+        for (int l = 0; l < PC; ++l) st[lane * PC + l] = acc[l];
+        wsync();
+        const uint64_t lim = (total - t0) * PC;
+        uint64_t *dst = E.out.limbs + t0 * PC;
+#pragma unroll
+        for (int r = 0; r < PC; ++r) {
+            const uint32_t j = lane + 64 * r;
+#if HM_ENC_NT
+            if (j < lim) __builtin_nontemporal_store(st[j], dst + j);
+#else
+            if (j < lim) dst[j] = st[j];
+#endif
+        }
+        wsync();
+    } else if (live) {
+        const uint32_t cap = cap_of(E.ob.b[k]);
+        uint64_t *dst = E.out.limbs + e * E.out.stride + E.ooff.b[k];
+#pragma unroll
+        for (int l = 0; l < PC; ++l) {
+            if ((uint32_t)l < cap) dst[l] = acc[l];
+            else if (acc[l]) flag(E.status, HM_ERR_CAPACITY);
+        }
+        for (uint32_t l = PC; l < cap; ++l) dst[l] = 0ull;
+    }
+}
+
+// tau = 128 (one 16-byte mask per ciphertext bit, 32 nibble groups): the lane's subset sum from its
+// mask mw, fully unrolled, then enc_finish
+template <int PC>
+__device__ __forceinline__ void enc_bits_t128(const EncArgs &E, const uint4 *tab4, uint64_t *st,
+                                              uint64_t t0, uint64_t total, uint32_t nbits,
+                                              const uint4 &mw) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool live = t0 + lane < total;
+    const uint64_t t = live ? t0 + lane : total - 1;
+    const uint64_t e = E.lognbits >= 0 ? t >> E.lognbits : t / nbits;
+    const uint32_t k = (uint32_t)(t - e * nbits);
+    uint32_t a32[2 * PC];
+#pragma unroll
+    for (int l = 0; l < 2 * PC; ++l) a32[l] = 0u;
+    const uint32_t ws[4] = {mw.x, mw.y, mw.z, mw.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int j = 0; j < 8; j += 2)
+            enc_lookup2<PC>(a32, tab4, 8 * w + j, (ws[w] >> (4 * j)) & 15u, (ws[w] >> (4 * j + 4)) & 15u);
+    uint64_t acc[PC];
+#pragma unroll
+    for (int l = 0; l < PC; ++l) acc[l] = (uint64_t)a32[2 * l] | ((uint64_t)a32[2 * l + 1] << 32);
+    enc_finish<PC>(E, acc, st, t0, total, live, e, k, nbits);
+}
+
+// Copies the key's nibble table (G groups) into the block's LDS
+template <int PC>
+__device__ __forceinline__ void enc_table_to_lds(const EncArgs &E, uint32_t G, uint64_t *tab) {
+    constexpr int NP = (PC + 1) / 2;
+    const uint32_t n16 = G * NP * 16; // 16-byte chunks
+    const uint4 *src = (const uint4 *)E.pk_tab;
+    uint4 *dst = (uint4 *)tab;
+    for (uint32_t f = threadIdx.x; f < n16; f += blockDim.x) dst[f] = src[f];
+    __syncthreads();
+}
+
 // GC: compile-time group count (tau/4) for the fully unrolled path with 16-byte-aligned masks
-// (tau = 128: one uint4 of mask per ciphertext bit), 0 = any tau
+// (tau = 128: one uint4 of mask per ciphertext bit, read one iteration ahead), 0 = any tau
 template <int PC, int GC>
 __global__ void __launch_bounds__(kEncBlock) encrypt_table_kernel(EncArgs E) {
     constexpr int NP = (PC + 1) / 2;  // limb pairs
     extern __shared__ uint64_t tab[]; // [G][NP][16][2] (upload_pk)
     const uint32_t G = GC ? GC : (E.tau + 3) / 4;
-    {
-        const uint32_t n16 = G * NP * 16; // 16-byte chunks
-        const uint4 *src = (const uint4 *)E.pk_tab;
-        uint4 *dst = (uint4 *)tab;
-        for (uint32_t f = threadIdx.x; f < n16; f += blockDim.x) dst[f] = src[f];
-    }
-    __syncthreads();
+    enc_table_to_lds<PC>(E, G, tab);
     const uint4 *tab4 = (const uint4 *)tab;
     uint64_t *stage = tab + (size_t)G * NP * 32; // [waves][64][PC] store transpose
+    uint64_t *st = stage + (size_t)(threadIdx.x & ~63u) * PC;
     const uint32_t nbits = E.nbytes * 8;
     const uint32_t mb = (E.tau + 7) / 8;
     const uint64_t total = E.n * nbits;
@@ -132,35 +215,26 @@ __global__ void __launch_bounds__(kEncBlock) encrypt_table_kernel(EncArgs E) {
     // the batch compute on a clamped index and are masked out of every store
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t lane = threadIdx.x & 63u;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); t0 < total;
-         t0 += step) {
-        const bool live = t0 + lane < total;
-        const uint64_t t = live ? t0 + lane : total - 1;
-        const uint64_t e = E.lognbits >= 0 ? t >> E.lognbits : t / nbits;
-        const uint32_t k = (uint32_t)(t - e * nbits);
-        const uint8_t *m = E.masks + t * mb;
-        uint64_t acc[2 * NP];
+    const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    if constexpr (GC != 0) {
+        static_assert(GC == 32, "GC: tau = 128");
+        const uint4 *m4 = (const uint4 *)E.masks;
+        uint4 mw = first < total ? m4[min(first + lane, total - 1)] : make_uint4(0, 0, 0, 0);
+        for (uint64_t t0 = first; t0 < total; t0 += step) {
+            const uint4 cur = mw;
+            if (t0 + step < total) mw = m4[min(t0 + step + lane, total - 1)]; // next iteration's
+            enc_bits_t128<PC>(E, tab4, st, t0, total, nbits, cur);
+        }
+    } else {
+        for (uint64_t t0 = first; t0 < total; t0 += step) {
+            const bool live = t0 + lane < total;
+            const uint64_t t = live ? t0 + lane : total - 1;
+            const uint64_t e = E.lognbits >= 0 ? t >> E.lognbits : t / nbits;
+            const uint32_t k = (uint32_t)(t - e * nbits);
+            const uint8_t *m = E.masks + t * mb;
+            uint64_t acc[2 * NP];
 #pragma unroll
-        for (int l = 0; l < 2 * NP; ++l) acc[l] = 0;
-        if constexpr (GC != 0) {
-            static_assert(GC % 32 == 0, "GC: whole uint4 mask words");
-            uint32_t a32[2 * PC];
-#pragma unroll
-            for (int l = 0; l < 2 * PC; ++l) a32[l] = 0u;
-#pragma unroll
-            for (int w4 = 0; w4 < GC / 32; ++w4) {
-                const uint4 mw = ((const uint4 *)m)[w4];
-                const uint32_t ws[4] = {mw.x, mw.y, mw.z, mw.w};
-#pragma unroll
-                for (int w = 0; w < 4; ++w)
-#pragma unroll
-                    for (int j = 0; j < 8; j += 2)
-                        enc_lookup2<PC>(a32, tab4, 32 * w4 + 8 * w + j, (ws[w] >> (4 * j)) & 15u,
-                                        (ws[w] >> (4 * j + 4)) & 15u);
-            }
-#pragma unroll
-            for (int l = 0; l < PC; ++l) acc[l] = (uint64_t)a32[2 * l] | ((uint64_t)a32[2 * l + 1] << 32);
-        } else {
+            for (int l = 0; l < 2 * NP; ++l) acc[l] = 0;
             for (uint32_t g0 = 0; g0 < G; g0 += 8) { // one 32-bit mask word = 8 nibbles
                 const uint32_t b0 = g0 / 2;           // first mask byte of this word
                 uint32_t bits;
@@ -175,50 +249,103 @@ __global__ void __launch_bounds__(kEncBlock) encrypt_table_kernel(EncArgs E) {
                 for (uint32_t j = 0; j < ng; ++j)
                     enc_lookup<NP>(acc, tab4, g0 + j, (bits >> (4 * j)) & 15u);
             }
+            enc_finish<PC>(E, acc, st, t0, total, live, e, k, nbits);
         }
-        // mask bits at or above tau select nothing: the table rows past tau are zero, and the
-        // reference reads exactly ceil(tau/8) bytes, bits >= tau unused (cipher.rs:105-110)
-        acc[0] ^= (E.data[e * E.nbytes + k / 8] >> (k % 8)) & 1u; // add_bool_assign (:112)
-        int deg = 0;
+    }
+}
+
+// ChaCha20 block blk of (key, nonce) (D. J. Bernstein's original layout: constants, 256-bit key,
+// 64-bit block counter, 64-bit nonce): keystream bytes 64 blk .. 64 blk + 63, little-endian words
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
+
+#define HM_QR(a, b, c, d)                                                                          \
+    a += b, d = rotl32(d ^ a, 16), c += d, b = rotl32(b ^ c, 12), a += b, d = rotl32(d ^ a, 8),   \
+    c += d, b = rotl32(b ^ c, 7)
+
+__device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint64_t blk, uint64_t nonce,
+                                               uint32_t (&x)[16]) {
+    uint32_t s[16];
+    s[0] = 0x61707865u, s[1] = 0x3320646eu, s[2] = 0x79622d32u, s[3] = 0x6b206574u;
 #pragma unroll
-        for (int l = 0; l < PC; ++l)
-            if (acc[l]) deg = l * 64 + 63 - __builtin_clzll(acc[l]);
-        if (live) {
-            if ((uint32_t)deg > E.ob.b[k]) flag(E.status, HM_ERR_CAPACITY);
-            E.out.degree[e * nbits + k] = (uint32_t)deg;
-        }
-        if (E.uniform_cap) {
-            // the wave's 64 bits own 64*PC consecutive output limbs (limb l of bit t at t*PC + l):
-            // transpose through LDS and store them coalesced (lane j writes limb j, j + 64, ...)
-            uint64_t *st = stage + (size_t)(threadIdx.x & ~63u) * PC;
+    for (int i = 0; i < 8; ++i) s[4 + i] = key[i];
+    s[12] = (uint32_t)blk, s[13] = (uint32_t)(blk >> 32);
+    s[14] = (uint32_t)nonce, s[15] = (uint32_t)(nonce >> 32);
 #pragma unroll
-            for (int l = 0; l < PC; ++l) st[lane * PC + l] = acc[l];
-            wsync();
-            const uint64_t lim = (total - t0) * PC;
-            uint64_t *dst = E.out.limbs + t0 * PC;
+    for (int i = 0; i < 16; ++i) x[i] = s[i];
 #pragma unroll
-            for (int r = 0; r < PC; ++r) {
-                const uint32_t j = lane + 64 * r;
-                if (j < lim) dst[j] = st[j];
-            }
-            wsync();
-        } else if (live) {
-            const uint32_t cap = cap_of(E.ob.b[k]);
-            uint64_t *dst = E.out.limbs + e * E.out.stride + E.ooff.b[k];
+    for (int r = 0; r < 10; ++r) {
+        HM_QR(x[0], x[4], x[8], x[12]);
+        HM_QR(x[1], x[5], x[9], x[13]);
+        HM_QR(x[2], x[6], x[10], x[14]);
+        HM_QR(x[3], x[7], x[11], x[15]);
+        HM_QR(x[0], x[5], x[10], x[15]);
+        HM_QR(x[1], x[6], x[11], x[12]);
+        HM_QR(x[2], x[7], x[8], x[13]);
+        HM_QR(x[3], x[4], x[9], x[14]);
+    }
 #pragma unroll
-            for (int l = 0; l < PC; ++l) {
-                if ((uint32_t)l < cap) dst[l] = acc[l];
-                else if (acc[l]) flag(E.status, HM_ERR_CAPACITY);
-            }
-            for (uint32_t l = PC; l < cap; ++l) dst[l] = 0ull;
+    for (int i = 0; i < 16; ++i) x[i] += s[i];
+}
+#undef HM_QR
+
+// Encryption with the masks drawn inside the kernel (hm_encrypt_batch without caller masks,
+// tau = 128): the mask of ciphertext bit t is keystream bytes 16 t .. 16 t + 15 -- exactly the
+// bytes rand_fill_kernel would have written to the mask buffer -- so a wave takes 256 bits at a
+// time: lane L computes keystream block T0/4 + L (the masks of bits T0 + 4L .. T0 + 4L + 3), the
+// blocks meet in the wave's LDS stage, each lane reads back the masks of its bits T0 + 64 i + L
+// (i = 0..3), and the four 64-bit slices run as in encrypt_table_kernel.  The masks never touch
+// HBM (512 B per u32 written and read back by the unfused path).  The nonce is read from device
+// memory; rand_bump_kernel advances it after the launch, as after a draw.
+__global__ void rand_bump_kernel(uint64_t *nonce);
+
+template <int PC>
+__global__ void __launch_bounds__(kEncBlock) encrypt_chacha_kernel(EncArgs E, RandArgs R) {
+    constexpr int NP = (PC + 1) / 2;
+    constexpr uint32_t kStageWords = 64 * PC > 512 ? 64 * PC : 512; // u64: 64 lanes x 64 B of keystream
+    extern __shared__ uint64_t tab[];
+    constexpr uint32_t G = 32;
+    enc_table_to_lds<PC>(E, G, tab);
+    const uint4 *tab4 = (const uint4 *)tab;
+    uint64_t *st = tab + (size_t)G * NP * 32 + (size_t)(threadIdx.x >> 6) * kStageWords;
+    const uint32_t nbits = E.nbytes * 8;
+    const uint64_t total = E.n * nbits;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nonce = *R.nonce;
+    const uint64_t wstep = (uint64_t)gridDim.x * (blockDim.x >> 6) * 256;
+    for (uint64_t T0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256;
+         T0 < total; T0 += wstep) {
+        uint32_t x[16];
+        chacha20_block(R.key, T0 / 4 + lane, nonce, x);
+        uint4 *s4 = (uint4 *)st;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s4[4 * lane + i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+        wsync();
+        uint4 mw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mw[i] = s4[64 * i + lane]; // bit T0 + 64 i + lane
+        wsync();
+#pragma unroll 1
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t t0 = T0 + 64 * i;
+            if (t0 >= total) break;
+            enc_bits_t128<PC>(E, tab4, st, t0, total, nbits, mw[i]);
         }
     }
 }
 
 template <int PC>
-static void launch_enc_pc(const EncArgs &E, void *stream) {
+static void launch_enc_pc(const EncArgs &E, const RandArgs *R, void *stream) {
     const uint64_t threads = E.n * E.nbytes * 8;
     const size_t tab = (size_t)((E.tau + 3) / 4) * ((PC + 1) / 2) * 16 * 16;
+    if (R) { // fused draw (the host checked tau == 128 and the table)
+        const size_t lds = tab + (size_t)(kEncBlock / 64) * 8 * (64 * PC > 512 ? 64 * PC : 512);
+        const uint64_t want = ((threads + 255) / 256 + kEncBlock / 64 - 1) / (kEncBlock / 64);
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
+        const uint64_t blocks = std::min<uint64_t>(want, (uint64_t)E.cus * per_cu);
+        hipLaunchKernelGGL((encrypt_chacha_kernel<PC>), dim3((unsigned)blocks), dim3(kEncBlock), lds,
+                           (hipStream_t)stream, E, *R);
+        return;
+    }
     const size_t lds = tab + (size_t)kEncBlock * PC * 8; // + the store transpose
     if (E.pk_tab && tab <= kEncTableBytes && lds <= 160 * 1024) { // one CU's LDS at most
         // a few resident blocks per CU, each striding over bits (the table copy is amortised)
@@ -238,29 +365,41 @@ static void launch_enc_pc(const EncArgs &E, void *stream) {
                        (hipStream_t)stream, E);
 }
 
-int launch_encrypt(const EncArgs &E, void *stream) {
+bool encrypt_fusable(const EncArgs &E) {
+    return E.tau == 128 && E.pk_tab && E.pk_cap >= 1 && E.pk_cap <= 17 &&
+           (size_t)32 * ((E.pk_cap + 1) / 2) * 256 + (size_t)(kEncBlock / 64) * 8 *
+                   (64 * E.pk_cap > 512 ? 64 * E.pk_cap : 512) <= 160 * 1024;
+}
+
+int launch_encrypt(const EncArgs &E, const RandArgs *R, void *stream) {
     if (E.n == 0) return 0;
+    if (R && !encrypt_fusable(E)) return HM_ERR_UNSUPPORTED;
     switch (E.pk_cap) {
-    case 1: launch_enc_pc<1>(E, stream); break;
-    case 2: launch_enc_pc<2>(E, stream); break;
-    case 3: launch_enc_pc<3>(E, stream); break;
-    case 4: launch_enc_pc<4>(E, stream); break;
-    case 5: launch_enc_pc<5>(E, stream); break;
-    case 6: launch_enc_pc<6>(E, stream); break;
-    case 7: launch_enc_pc<7>(E, stream); break;
-    case 8: launch_enc_pc<8>(E, stream); break;
-    case 9: launch_enc_pc<9>(E, stream); break;
-    case 10: launch_enc_pc<10>(E, stream); break;
-    case 11: launch_enc_pc<11>(E, stream); break;
-    case 12: launch_enc_pc<12>(E, stream); break;
-    case 13: launch_enc_pc<13>(E, stream); break;
-    case 14: launch_enc_pc<14>(E, stream); break;
-    case 15: launch_enc_pc<15>(E, stream); break;
-    case 16: launch_enc_pc<16>(E, stream); break;
-    case 17: launch_enc_pc<17>(E, stream); break;
+    case 1: launch_enc_pc<1>(E, R, stream); break;
+    case 2: launch_enc_pc<2>(E, R, stream); break;
+    case 3: launch_enc_pc<3>(E, R, stream); break;
+    case 4: launch_enc_pc<4>(E, R, stream); break;
+    case 5: launch_enc_pc<5>(E, R, stream); break;
+    case 6: launch_enc_pc<6>(E, R, stream); break;
+    case 7: launch_enc_pc<7>(E, R, stream); break;
+    case 8: launch_enc_pc<8>(E, R, stream); break;
+    case 9: launch_enc_pc<9>(E, R, stream); break;
+    case 10: launch_enc_pc<10>(E, R, stream); break;
+    case 11: launch_enc_pc<11>(E, R, stream); break;
+    case 12: launch_enc_pc<12>(E, R, stream); break;
+    case 13: launch_enc_pc<13>(E, R, stream); break;
+    case 14: launch_enc_pc<14>(E, R, stream); break;
+    case 15: launch_enc_pc<15>(E, R, stream); break;
+    case 16: launch_enc_pc<16>(E, R, stream); break;
+    case 17: launch_enc_pc<17>(E, R, stream); break;
     default: return HM_ERR_UNSUPPORTED;
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (R) { // the draw consumed this nonce's keystream
+        hipLaunchKernelGGL(rand_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, R->nonce);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -383,41 +522,14 @@ int launch_decrypt(const DecArgs &D, void *stream) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Device CSPRNG for encryption masks: ChaCha20 (D. J. Bernstein's original layout: constants,
-// 256-bit key, 64-bit block counter, 64-bit nonce), one 64-byte block per thread.  The nonce is
-// read from device memory and advanced by rand_bump_kernel after the draw, so a graph replay
-// never repeats a keystream.
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
-
-#define HM_QR(a, b, c, d)                                                                          \
-    a += b, d = rotl32(d ^ a, 16), c += d, b = rotl32(b ^ c, 12), a += b, d = rotl32(d ^ a, 8),   \
-    c += d, b = rotl32(b ^ c, 7)
-
+// Device CSPRNG for encryption masks: ChaCha20 (chacha20_block above), one 64-byte block per
+// thread.  The nonce is read from device memory and advanced by rand_bump_kernel after the draw,
+// so a graph replay never repeats a keystream.
 __global__ void __launch_bounds__(256) rand_fill_kernel(RandArgs R) {
     const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (blk * 64 >= R.nbytes) return;
-    const uint64_t nonce = *R.nonce;
-    uint32_t x[16], s[16];
-    s[0] = 0x61707865u, s[1] = 0x3320646eu, s[2] = 0x79622d32u, s[3] = 0x6b206574u;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[4 + i] = R.key[i];
-    s[12] = (uint32_t)blk, s[13] = (uint32_t)(blk >> 32);
-    s[14] = (uint32_t)nonce, s[15] = (uint32_t)(nonce >> 32);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = s[i];
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        HM_QR(x[0], x[4], x[8], x[12]);
-        HM_QR(x[1], x[5], x[9], x[13]);
-        HM_QR(x[2], x[6], x[10], x[14]);
-        HM_QR(x[3], x[7], x[11], x[15]);
-        HM_QR(x[0], x[5], x[10], x[15]);
-        HM_QR(x[1], x[6], x[11], x[12]);
-        HM_QR(x[2], x[7], x[8], x[13]);
-        HM_QR(x[3], x[4], x[9], x[14]);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] += s[i];
+    uint32_t x[16];
+    chacha20_block(R.key, blk, *R.nonce, x);
     uint8_t *dst = R.out + blk * 64;
     if (blk * 64 + 64 <= R.nbytes && ((uintptr_t)dst & 15u) == 0) {
         uint4 *d4 = (uint4 *)dst;
@@ -428,7 +540,6 @@ __global__ void __launch_bounds__(256) rand_fill_kernel(RandArgs R) {
             dst[k] = (uint8_t)(x[k / 4] >> (8 * (k % 4)));
     }
 }
-#undef HM_QR
 
 __global__ void rand_bump_kernel(uint64_t *nonce) {
     if (threadIdx.x == 0) atomicAdd((unsigned long long *)nonce, 1ull);

@@ -296,7 +296,10 @@ int launch_add_prep(const AddArgs &a, void *stream);
 AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n);
 int launch_add_chain_mfma(const AddArgs &a, void *stream);
 int launch_add_chain_valu(const AddArgs &a, void *stream);
-int launch_encrypt(const EncArgs &a, void *stream);
+// R: draw the masks inside the kernel from R's ChaCha20 stream (masks == null; tau = 128 only,
+// encrypt_fusable) and advance R's nonce, instead of reading a.masks
+int launch_encrypt(const EncArgs &a, const RandArgs *R, void *stream);
+bool encrypt_fusable(const EncArgs &a);
 int launch_decrypt(const DecArgs &a, void *stream);
 int launch_gate(const GateArgs &a, void *stream);
 int launch_mul_stage(const MulStageArgs &a, void *stream);

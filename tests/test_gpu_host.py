@@ -3,7 +3,7 @@ shape (context.rs:555-595 examples), captured-graph validity across buffer chang
 import numpy as np
 import pytest
 
-from helpers import as_bytes, assert_batches_equal, masks, plain, seeded_random_bytes
+from helpers import as_bytes, assert_batches_equal, masks, plain, seeded_value_masks
 
 pytestmark = pytest.mark.gpu
 
@@ -50,23 +50,33 @@ def test_unseeded_keys_and_masks_are_fresh(H):
     assert np.array_equal(c1.decrypt(e1), x) and np.array_equal(c1.decrypt(e2), x)
 
 
-def test_engine_masks_reproduce_with_seed(H, oracle):
+@pytest.mark.parametrize("params,dtype,n", [((64, 64, 1, 64), np.uint16, 40),
+                                            ((128, 128, 1, 128), np.uint32, 41),
+                                            ((128, 128, 1, 128), np.uint32, 40000)])
+def test_engine_masks_reproduce_with_seed(H, oracle, params, dtype, n):
     """Engine-drawn masks under a seed are the seeded ChaCha20 bytes: the oracle, fed those
-    bytes, produces the identical ciphertexts."""
-    params = (64, 64, 1, 64)
+    bytes, produces the identical ciphertexts.  At tau = 128 the masks are drawn inside the
+    encryption kernel (encrypt_chacha_kernel: 256 bits per wave, a partial last slice at
+    n = 41; n = 40000 takes several grid strides, checked on sampled values); the second
+    encryption uses the next nonce."""
     ctx = H.Context(H.Parameters(*params))
     ctx.seed_rng(77)
     ctx.generate_secret_key()
     ctx.generate_public_key()
-    x = plain(40, np.uint16, 3)
-    c = ctx.encrypt(x)  # first mask draw of this context
-    ctx.synchronize()
-    m = seeded_random_bytes(77, 0, 40 * 16 * ctx.mask_bytes()).reshape(40, 16, -1)
+    nbits = 8 * np.dtype(dtype).itemsize
     pk = ctx.get_public_key().limbs
-    bound = c.bound
-    rl, rd = oracle.encrypt_batch(pk, as_bytes(x), m, bound)
-    gl, gd = c.to_host()
-    assert_batches_equal(gl, gd, rl, rd, bound, 40, "engine-mask encrypt")
+    for draw in range(2):
+        x = plain(n, dtype, 3 + draw)
+        c = ctx.encrypt(x)  # draw `draw` of this context
+        ctx.synchronize()
+        idx = np.arange(n) if n <= 64 else np.array([0, 1, 7, 8191, 8192, 12345, 32767, 32768, n - 1])
+        m = seeded_value_masks(77, draw, idx, nbits, ctx.mask_bytes())
+        rl, rd = oracle.encrypt_batch(pk, as_bytes(x[idx]), m, c.bound)
+        gl, gd = c.to_host()
+        gl = gl.reshape(n, -1)[idx].reshape(-1)
+        gd = gd.reshape(n, -1)[idx].reshape(-1)
+        assert_batches_equal(gl, gd, rl, rd, c.bound, len(idx), f"engine-mask encrypt, draw {draw}")
+        assert np.array_equal(ctx.decrypt(c), x)
 
 
 def test_loaded_secret_key_of_high_degree(H, oracle):
