@@ -359,6 +359,13 @@ hm_status hm_ctx_set_public_key(hm_ctx *c, const uint64_t *limbs, uint32_t tau, 
     c->pk_maxdeg = 0;
     for (uint32_t i = 0; i < tau; ++i)
         c->pk_maxdeg = std::max<uint32_t>(c->pk_maxdeg, (uint32_t)degree_of(&c->pk[(size_t)i * lpp], lpp));
+    c->pk_top1 = tau <= 128 && lpp > 1;
+    std::memset(c->pk_topcol, 0, sizeof(c->pk_topcol));
+    for (uint32_t i = 0; i < tau && c->pk_top1; ++i) {
+        const uint64_t top = c->pk[(size_t)i * lpp + lpp - 1];
+        if (top > 1) c->pk_top1 = false;
+        else c->pk_topcol[i / 32] |= (uint32_t)top << (i % 32);
+    }
     hm_status st = upload_pk(c);
     if (st == HM_OK) c->has_pk = true;
     return st;
@@ -624,6 +631,10 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
         E.ooff.b[i] = o, o += cap_of(out->bound[i]);
         E.uniform_cap &= cap_of(out->bound[i]) == c->pk_cap;
     }
+#ifndef HM_ENC_NO_TOP1
+    E.top1 = c->pk_top1 ? 1u : 0u;
+#endif
+    std::memcpy(E.topcol, c->pk_topcol, sizeof(E.topcol));
     if (!masks && encrypt_fusable(E)) {
         // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): the device
         // ChaCha20 stream, drawn inside the encryption kernel (the same keystream bytes a draw into

@@ -32,6 +32,9 @@ struct hm_ctx {
     std::vector<uint64_t> pk;          // tau * pk_cap limbs
     uint32_t pk_tau = 0, pk_cap = 0;
     uint32_t pk_maxdeg = 0;
+    // the rows' top limbs are all 0 or 1 (tau <= 128): their bits as a column (EncArgs::topcol)
+    bool pk_top1 = false;
+    uint32_t pk_topcol[4] = {0, 0, 0, 0};
     // device state
     uint64_t *d_pk = nullptr;
     uint64_t *d_pk_tab = nullptr;      // encryption nibble table (upload_pk), or null

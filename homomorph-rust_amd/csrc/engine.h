@@ -62,6 +62,10 @@ struct EncArgs {
     int *status;
     Bounds ob;
     Bounds ooff;            // limb offset of each bit within a value (prefix sums of the caps)
+    // every row's top limb (pk_cap - 1) is 0 or 1 (tau <= 128): that limb of a subset sum is
+    // parity(mask & topcol), topcol bit i = row i's bit 64 (pk_cap - 1) (cipher.hip enc_bits_t128)
+    uint32_t top1;
+    uint32_t topcol[4];
 };
 
 struct DecArgs {
