@@ -208,6 +208,25 @@ hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n) {
 
 } // namespace
 
+// The context's auxiliary stream and its fork / mid / join events (the add pipeline, the
+// multiplier's second Karatsuba lane), created on first use into locals and stored only when all
+// of them exist.
+hm_status hm::ensure_aux_stream(hm_ctx *c) {
+    if (c->aux_stream) return HM_OK;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        for (hipEvent_t x : ev)
+            if (x) (void)hipEventDestroy(x);
+        if (s) (void)hipStreamDestroy(s);
+        return hip_fail(c, e);
+    }
+    c->aux_stream = s, c->ev_fork = ev[0], c->ev_mid = ev[1], c->ev_join = ev[2];
+    return HM_OK;
+}
+
 // The status an hm_* entry returns for the exception its function-try-block caught (HM_ABI_CATCH,
 // ctx.h): host containers throw std::bad_alloc; nothing is allowed to unwind into a C, Rust or
 // ctypes caller.
@@ -815,20 +834,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     // halves use disjoint workspace and outputs.  Fork / join by events, so a graph captured on
     // the context stream holds both branches.
     if (c->add_pipe && !c->time_chain && A.mfma && a->n >= 2 * kAddPipeMin) {
-        if (!c->aux_stream) { // created into locals, stored only when all of them exist
-            hipStream_t s = nullptr;
-            hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-            hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-            for (int k = 0; k < 3 && e == hipSuccess; ++k)
-                e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
-            if (e != hipSuccess) {
-                for (hipEvent_t x : ev)
-                    if (x) (void)hipEventDestroy(x);
-                if (s) (void)hipStreamDestroy(s);
-                return hip_fail(c, e);
-            }
-            c->aux_stream = s, c->ev_fork = ev[0], c->ev_mid = ev[1], c->ev_join = ev[2];
-        }
+        if (hm_status st = ensure_aux_stream(c); st) return st;
         const uint64_t h = (a->n / 2 + kAddWavesPerBlock - 1) / kAddWavesPerBlock * kAddWavesPerBlock;
         const AddArgs A1 = add_args_slice(A, 0, h), A2 = add_args_slice(A, h, a->n - h);
         HM_HIP(c, hipEventRecord(c->ev_fork, c->stream));

@@ -146,6 +146,7 @@ inline hm_status hip_fail(hm_ctx *c, hipError_t e) {
 // exception (std::bad_alloc from a host container above all) crosses the C ABI
 // (include/homomorph_gpu.h: HM_ERR_OUT_OF_MEMORY, HM_ERR_INTERNAL).
 hm_status exception_status() noexcept;
+hm_status ensure_aux_stream(hm_ctx *c);
 #define HM_ABI_CATCH                                                                              \
     catch (...) {                                                                                 \
         return hm::exception_status();                                                            \

@@ -25,6 +25,13 @@ namespace hm {
 namespace {
 
 constexpr int64_t kBoundLimit = (int64_t)1 << 30;
+// Karatsuba lanes: a column's Karatsuba products alternate between two scratch regions and two
+// streams (the context stream and its auxiliary stream), so one product's HBM-bound operand sums
+// and recombinations, and the tail of its leaf launch, overlap the next product's leaves
+#ifndef HM_KA_LANES
+#define HM_KA_LANES 2
+#endif
+constexpr uint32_t kKaLanes = HM_KA_LANES;
 constexpr uint32_t kNW = sizeof(kMulTileW) / sizeof(kMulTileW[0]);
 // schoolbook products whose uniform operand has at least this many words run on the matrix cores
 // (mfma plans); narrower ones keep the VALU tiles
@@ -47,6 +54,7 @@ inline bool pp_flip(bool is_signed, uint32_t L, uint32_t i, uint32_t j) {
 // One Karatsuba product (see "Karatsuba" below): its launches, in order.
 struct KaProg {
     uint32_t u, v, out;                          // slots (exact degrees: deg1)
+    uint32_t lane = 0;                           // scratch region / stream (mul_columns)
     std::vector<std::array<uint32_t, 3>> sums;   // per level 1..k: (first KaSum, count, h)
     uint32_t vtask = 0, nvtask = 0;              // leaf products (MulVTask range)
     uint32_t leaf_umax = 0, leaf_vmax = 0, leaf_omax = 0; // their largest operands and output
@@ -205,7 +213,7 @@ struct KaBuild {
 // even columns / carries of odd columns); regions are placed once their maxima are known.
 bool build_plan(MulPlan &P) {
     const uint32_t K = P.K;
-    enum { IN, PP, PRE, CA, CB, KA, PPA, NREG };
+    enum { IN, PP, PRE, CA, CB, KA, PPA, KA2, NREG };
     Region reg[NREG];
     std::vector<uint8_t> slot_reg;
     auto new_slot = [&](int r, int64_t bound) -> uint32_t {
@@ -332,6 +340,7 @@ bool build_plan(MulPlan &P) {
         // Karatsuba for the big products (their slots are final now: region offsets are fixed
         // when the regions are placed, so views are recorded relative and fixed up below)
         std::vector<bool> is_ka(P.prod.size() - col.prod, false);
+        uint32_t nka = 0; // this column's Karatsuba products so far: they alternate lanes
         for (uint32_t k = col.prod; k < P.prod.size() && P.ka_min; ++k) {
             const MulProdTask &T = P.prod[k];
             const uint32_t nu = P.slots[T.u].words, nv = P.slots[T.v].words;
@@ -342,14 +351,18 @@ bool build_plan(MulPlan &P) {
             // leaf: the smallest multiple of 32 words with leaf * 2^lk >= max(nu, nv)
             const uint32_t mx = std::max(nu, nv);
             const uint32_t leaf = (((mx + (1u << lk) - 1) >> lk) + 31) & ~31u;
-            KaBuild kb{(uint32_t)KA, leaf};
+            // two lanes (kKaLanes): products alternate between two scratch regions, so that
+            // mul_columns can run consecutive products on two streams
+            const uint32_t lane = kKaLanes > 1 ? (nka++ & 1u) : 0u;
+            KaBuild kb{(uint32_t)(lane ? KA2 : KA), leaf};
             auto view = [&](uint32_t slot) {
                 return ((uint32_t)slot_reg[slot] << kRegShift) | P.slots[slot].off;
             };
             kb.node(0, view(T.u), nu, view(T.v), nv, leaf << lk, view(T.out), P.slots[T.out].words);
-            reg[KA].max = std::max(reg[KA].max, kb.max);
+            reg[lane ? KA2 : KA].max = std::max(reg[lane ? KA2 : KA].max, kb.max);
             KaProg pg;
             pg.u = T.u, pg.v = T.v, pg.out = T.out;
+            pg.lane = lane;
             for (uint32_t l = 0; l < kb.sums.size(); ++l) {
                 if (kb.sums[l].empty()) continue;
                 pg.sums.push_back({(uint32_t)P.ka_sums.size(), (uint32_t)kb.sums[l].size(),
@@ -596,12 +609,12 @@ namespace {
 
 // the launches of one Karatsuba product: sums by depth, leaf products, recombination bottom-up,
 // and the exact output degree
-hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B) {
+hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B, hipStream_t st) {
     const uint8_t *T = P.d_tab;
     for (const auto &lv : pg.sums) {
         KaSumArgs a{};
         a.B = B, a.t = (const KaSum *)(T + P.off_ka_sums) + lv[0], a.nt = lv[1], a.h = lv[2];
-        if (launch_ka_sum(a, c->stream)) return hip_fail(c, hipGetLastError());
+        if (launch_ka_sum(a, st)) return hip_fail(c, hipGetLastError());
     }
     if (P.mfma) {
         // the leaves on the matrix cores: one wave per (value, leaf)
@@ -617,24 +630,24 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         const uint32_t lw = mul_mfma_lean_leaf_wave_words(a.vmax, a.span, a.umax);
         if (a.umax <= kMfLeanLeafWords && (256 + 4 * (size_t)lw) * 4 * 4 <= 160 * 1024)
             a.lean = 1, a.wave_words = lw;
-        if (launch_mul_mfma(a, true, c->stream)) return hip_fail(c, hipGetLastError());
+        if (launch_mul_mfma(a, true, st)) return hip_fail(c, hipGetLastError());
     } else {
         for (uint32_t q = 0; q < kNW; ++q) {
             if (!pg.ntiles[q]) continue;
             MulVProdArgs a{};
             a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
             a.tiles = (const MulVTile *)(T + P.off_ka_vtiles) + pg.tiles[q], a.ntiles = pg.ntiles[q];
-            if (launch_mul_vprod(a, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
+            if (launch_mul_vprod(a, kMulTileW[q], st)) return hip_fail(c, hipGetLastError());
         }
     }
     for (const auto &lv : pg.combs) {
         KaCombArgs a{};
         a.B = B, a.t = (const KaComb *)(T + P.off_ka_combs) + lv[0], a.nt = lv[1], a.h = lv[2];
-        if (launch_ka_comb(a, c->stream)) return hip_fail(c, hipGetLastError());
+        if (launch_ka_comb(a, st)) return hip_fail(c, hipGetLastError());
     }
     MulDegArgs d{};
     d.B = B, d.u = pg.u, d.v = pg.v, d.out = pg.out;
-    if (launch_mul_deg(d, c->stream)) return hip_fail(c, hipGetLastError());
+    if (launch_mul_deg(d, st)) return hip_fail(c, hipGetLastError());
     return HM_OK;
 }
 
@@ -728,8 +741,23 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 pr.ntiles = col.ntiles[q];
                 if (launch_mul_prod(pr, kMulTileW[q], c->stream)) return hip_fail(c, hipGetLastError());
             }
-            for (const KaProg &pg : col.ka) // one Karatsuba product at a time (shared scratch)
-                if (hm_status st = run_ka(c, *P, pg, B); st) return st;
+            // Karatsuba products: lane 0 on the context stream, lane 1 on the auxiliary stream
+            // (each lane's products one at a time: they share the lane's scratch region); the
+            // lanes fork after this column's scan and schoolbook launches (the products read its
+            // prefixes) and join before the next column's scan (which reads their carries)
+            const bool two = col.ka.size() > 1 && kKaLanes > 1;
+            if (two) {
+                if (hm_status st = ensure_aux_stream(c); st) return st;
+                HM_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+                HM_HIP(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+            }
+            for (const KaProg &pg : col.ka)
+                if (hm_status st = run_ka(c, *P, pg, B, two && pg.lane ? c->aux_stream : c->stream); st)
+                    return st;
+            if (two) {
+                HM_HIP(c, hipEventRecord(c->ev_join, c->aux_stream));
+                HM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+            }
         }
         MulFinalArgs F{};
         F.B = B, F.res = (const uint32_t *)(T + P->off_res), F.K = K, F.out = oa;
