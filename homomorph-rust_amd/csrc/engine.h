@@ -167,6 +167,9 @@ struct KaSumArgs {
 struct MulVTask {
     uint32_t u, nu, v, nv; // operand views (nu, nv valid words; 0 = null)
     uint32_t out, nout;    // out[0:nout) = U * V
+    // MFMA leaves of the deepest Karatsuba level read a sum operand lo + hi as two views:
+    // U = u[0:nu) ^ u2[0:nu2) (nu2 <= nu; nu2 = 0: no second view), the same for V
+    uint32_t u2, nu2, v2, nv2;
 };
 struct MulVTile {
     uint32_t task, base;

@@ -32,6 +32,12 @@ constexpr int64_t kBoundLimit = (int64_t)1 << 30;
 #define HM_KA_LANES 2
 #endif
 constexpr uint32_t kKaLanes = HM_KA_LANES;
+// the deepest Karatsuba level's operand sums (lo + hi) are not formed in HBM by ka_sum_kernel:
+// the MFMA leaves read both halves and XOR them while building their operand images
+#ifndef HM_KA_FUSE_SUMS
+#define HM_KA_FUSE_SUMS 1
+#endif
+constexpr bool kFuseLeafSums = HM_KA_FUSE_SUMS;
 constexpr uint32_t kNW = sizeof(kMulTileW) / sizeof(kMulTileW[0]);
 // schoolbook products whose uniform operand has at least this many words run on the matrix cores
 // (mfma plans); narrower ones keep the VALU tiles
@@ -150,6 +156,7 @@ constexpr uint32_t kRegShift = 28, kRelMask = (1u << kRegShift) - 1;
 
 struct KaBuild {
     uint32_t ka_region, leaf;
+    bool fuse_leaf_sums = false; // the deepest level's sums are read by the leaves (MFMA plans)
     uint64_t top = 0, max = 0; // scratch bump allocator in the KA region (words)
     std::vector<std::vector<KaSum>> sums;   // by split depth
     std::vector<std::vector<KaComb>> combs; // by split depth
@@ -162,10 +169,13 @@ struct KaBuild {
         return (ka_region << kRegShift) | (uint32_t)o;
     }
     // r[0:min(2n, rcap)) = U * V for views u (un valid words), v (vn), both of logical size n
+    // u2 / v2 (nu2 / nv2 valid words): a second view XORed into the operand (fused leaf sums)
     void node(uint32_t lvl, uint32_t uo, uint32_t un, uint32_t vo, uint32_t vn, uint32_t n,
-              uint32_t r, uint32_t rcap) {
+              uint32_t r, uint32_t rcap, uint32_t u2 = kKaNone, uint32_t nu2 = 0,
+              uint32_t v2 = kKaNone, uint32_t nv2 = 0) {
         if (n == leaf) {
-            leaves.push_back({uo, std::min(un, n), vo, std::min(vn, n), r, std::min(2 * n, rcap)});
+            leaves.push_back({uo, std::min(un, n), vo, std::min(vn, n), r, std::min(2 * n, rcap),
+                              u2, std::min(nu2, n), v2, std::min(nv2, n)});
             return;
         }
         const uint32_t h = n / 2;
@@ -180,7 +190,10 @@ struct KaBuild {
         }
         struct Half {
             uint32_t lo_n, hi_o, hi_n, s_o, s_n;
+            uint32_t s2_o = kKaNone, s2_n = 0; // (fused leaf sums) the sum's second view
         };
+        // children that are leaves read lo + hi as two views instead of a formed sum
+        const bool fuse = fuse_leaf_sums && h == leaf;
         auto half = [&](uint32_t o, uint32_t len) {
             Half x;
             x.lo_n = std::min(len, h);
@@ -188,6 +201,8 @@ struct KaBuild {
             x.hi_n = len > h ? len - h : 0u;
             if (x.hi_n == 0) { // lo + hi = lo: no sum to form
                 x.s_o = o, x.s_n = x.lo_n;
+            } else if (fuse) { // lo_n = h >= hi_n
+                x.s_o = o, x.s_n = x.lo_n, x.s2_o = x.hi_o, x.s2_n = x.hi_n;
             } else {
                 x.s_o = alloc(h), x.s_n = h;
                 if (sums.size() <= lvl) sums.resize(lvl + 1);
@@ -201,7 +216,7 @@ struct KaBuild {
         const uint32_t z1 = has_z1 ? alloc(2 * h) : kKaNone;
         node(lvl + 1, uo, U.lo_n, vo, V.lo_n, h, z0, 2 * h);
         if (has_z1) node(lvl + 1, U.hi_o, U.hi_n, V.hi_o, V.hi_n, h, z1, 2 * h);
-        node(lvl + 1, U.s_o, U.s_n, V.s_o, V.s_n, h, z2, 2 * h);
+        node(lvl + 1, U.s_o, U.s_n, V.s_o, V.s_n, h, z2, 2 * h, U.s2_o, U.s2_n, V.s2_o, V.s2_n);
         if (combs.size() <= lvl) combs.resize(lvl + 1);
         combs[lvl].push_back({z0, z1, z2, r, rcap});
     }
@@ -355,6 +370,7 @@ bool build_plan(MulPlan &P) {
             // mul_columns can run consecutive products on two streams
             const uint32_t lane = kKaLanes > 1 ? (nka++ & 1u) : 0u;
             KaBuild kb{(uint32_t)(lane ? KA2 : KA), leaf};
+            kb.fuse_leaf_sums = P.mfma && kFuseLeafSums;
             auto view = [&](uint32_t slot) {
                 return ((uint32_t)slot_reg[slot] << kRegShift) | P.slots[slot].off;
             };
@@ -457,7 +473,8 @@ bool build_plan(MulPlan &P) {
         return o == kKaNone ? o : (uint32_t)(reg[o >> kRegShift].base + (o & kRelMask));
     };
     for (auto &t : P.ka_sums) t.src = fix(t.src), t.dst = fix(t.dst);
-    for (auto &t : P.ka_vtasks) t.u = fix(t.u), t.v = fix(t.v), t.out = fix(t.out);
+    for (auto &t : P.ka_vtasks)
+        t.u = fix(t.u), t.v = fix(t.v), t.out = fix(t.out), t.u2 = fix(t.u2), t.v2 = fix(t.v2);
     for (auto &t : P.ka_combs) t.z0 = fix(t.z0), t.z1 = fix(t.z1), t.z2 = fix(t.z2), t.r = fix(t.r);
     P.astride = std::max<uint64_t>(base, 4);
     return true;

@@ -129,11 +129,14 @@ __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI,
 }
 
 // RS quad R-1-q = the nibbles of bitreverse(U[q]) for q < ub, zero up to R, then zero to rs_words
+// (U2: a second view XORed in below ub2, a fused Karatsuba sum; ub2 <= 0: none)
 __device__ __forceinline__ void mf_u_image(const uint32_t *U, int ub, int R, uint32_t rs_words,
-                                           const uint32_t *tab, uint32_t *RS) {
+                                           const uint32_t *tab, uint32_t *RS,
+                                           const uint32_t *U2 = nullptr, int ub2 = 0) {
     const int lane = lane_id();
     for (int q = lane; q < R; q += kWave) {
-        const uint32_t rev = q < ub ? __builtin_bitreverse32(U[q]) : 0u;
+        const uint32_t rev =
+            q < ub ? __builtin_bitreverse32(U[q] ^ (q < ub2 ? U2[q] : 0u)) : 0u;
         uint4 x;
         x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
         x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
@@ -144,11 +147,12 @@ __device__ __forceinline__ void mf_u_image(const uint32_t *U, int ub, int R, uin
 
 // VI quad i = the nibbles of V word vlo + i (zero outside [0, nv)) for i < vhi - vlo
 __device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, int vhi,
-                                           const uint32_t *tab, uint32_t *VI) {
+                                           const uint32_t *tab, uint32_t *VI,
+                                           const uint32_t *V2 = nullptr, int nv2 = 0) {
     const int lane = lane_id();
     for (int i = lane; i < vhi - vlo; i += kWave) {
         const int w = vlo + i;
-        const uint32_t v = (w >= 0 && w < nv) ? V[w] : 0u;
+        const uint32_t v = (w >= 0 && w < nv) ? V[w] ^ (w < nv2 ? V2[w] : 0u) : 0u;
         uint4 q;
         q.x = tab[v & 0xFFu], q.y = tab[(v >> 8) & 0xFFu];
         q.z = tab[(v >> 16) & 0xFFu], q.w = tab[v >> 24];
@@ -161,10 +165,11 @@ __device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, i
 // Qlo + 2G + 1, i.e. U words q = R - 1 - Q (zero outside [0, ub)), are all its fragments read
 __host__ __device__ constexpr uint32_t mf_win_words(int G) { return 4u * (2u * (uint32_t)G + 2u) + 16u; }
 // lane k's U word of the window of the group of G chunks from c0 (k < 2G + 2 <= 36 lanes)
-__device__ __forceinline__ uint32_t mf_win_word(const uint32_t *Ub, int ub, int R, int c0, int G) {
+__device__ __forceinline__ uint32_t mf_win_word(const uint32_t *Ub, int ub, int R, int c0, int G,
+                                                const uint32_t *Ub2, int ub2) {
     const int lane = lane_id();
     const int q = R - 1 - (2 * c0 + 1 + lane);
-    return (lane < 2 * G + 2 && q >= 0 && q < ub) ? Ub[q] : 0u;
+    return (lane < 2 * G + 2 && q >= 0 && q < ub) ? Ub[q] ^ (q < ub2 ? Ub2[q] : 0u) : 0u;
 }
 // wword: this lane's window word (mf_win_word, loaded ahead); the next group's is loaded here,
 // before the sweep, into *next (G2 chunks from c0 + G; G2 = 0: none)
@@ -172,7 +177,8 @@ template <int G>
 __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub, int ub, int G2,
                                              uint32_t *next, uint32_t *RSW, const uint32_t *tab,
                                              const uint32_t *VI, int vlo, int R, int D, int nv,
-                                             int Ts, int Te, int c0, uint32_t *OUT) {
+                                             int Ts, int Te, int c0, uint32_t *OUT,
+                                             const uint32_t *Ub2, int ub2) {
     const int lane = lane_id();
     const int Qlo = 2 * c0 + 1;
     wsync(); // the previous group's fragment reads are done
@@ -186,7 +192,7 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
     wsync();
     v8i Af[G];
     mf_afrags<G>(RSW - 4 * Qlo, R, D, c0, Af);
-    if (G2) *next = mf_win_word(Ub, ub, R, c0 + G, G2);
+    if (G2) *next = mf_win_word(Ub, ub, R, c0 + G, G2, Ub2, ub2);
     mf_sweep<G, false>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
 }
 
@@ -222,14 +228,17 @@ mul_mfma_kernel(MulMfmaArgs P) {
     if (e >= P.B.nv) return; // whole wave exits together
     const uint32_t item = (uint32_t)(g % P.nitems);
     uint32_t *arena = P.B.arena + e * P.B.astride;
-    const uint32_t *U, *V;
+    const uint32_t *U, *V, *U2 = nullptr, *V2 = nullptr;
     uint32_t *O;
-    int nu, nv, nout, base;
+    int nu, nv, nout, base, nu2 = 0, nv2 = 0;
     if constexpr (LEAF) {
         const MulVTask t = ((const MulVTask *)P.tasks)[item / P.nspans];
         base = (int)(item % P.nspans) * 32 * (int)P.span;
         U = arena + t.u, V = arena + t.v, O = arena + t.out;
         nu = (int)rfl(t.nu), nv = (int)rfl(t.nv), nout = (int)rfl(t.nout);
+        // a fused Karatsuba sum: the operand is u ^ u2 (second view nu2 <= nu words)
+        nu2 = (int)rfl(t.nu2), nv2 = (int)rfl(t.nv2);
+        U2 = arena + (nu2 ? t.u2 : t.u), V2 = arena + (nv2 ? t.v2 : t.v);
         if (base >= nout) return;
     } else {
         const MulTile tl = P.spans[item];
@@ -243,6 +252,8 @@ mul_mfma_kernel(MulMfmaArgs P) {
         if (base == 0 && lane_id() == 0)
             P.B.deg1[(uint64_t)t.out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
     }
+    if (!nu2) U2 = U; // (never read: a valid pointer all the same)
+    if (!nv2) V2 = V;
     const int lane = lane_id();
     const int span = (int)P.span;
     const int wend = min(nout, base + 32 * span); // this span's output words [base, wend)
@@ -267,8 +278,8 @@ mul_mfma_kernel(MulMfmaArgs P) {
         const int vhi = min(32 * Te + 32 - D + 2 * nc, nv + kVPad);
         wsync(); // the previous block's reads of RS / VI are done
         // RS quad R-1-q = the nibbles of bitreverse(U_b[q]) (one load, one 16-B store per word)
-        if constexpr (!WIN) mf_u_image(U + b0, ub, R, rs_words, tab, RS);
-        mf_v_image(V, nv, vlo, vhi, tab, VI);
+        if constexpr (!WIN) mf_u_image(U + b0, ub, R, rs_words, tab, RS, U2 + b0, nu2 - b0);
+        mf_v_image(V, nv, vlo, vhi, tab, VI, V2, nv2);
         wsync();
         const int tlo = max(Ts, 0);
         uint32_t *OUTs = OUT + 32 * (tlo - Ts);
@@ -279,18 +290,19 @@ mul_mfma_kernel(MulMfmaArgs P) {
         int c0 = 0;
         // (lean leaves) each group's U window words are loaded one group ahead
         auto gsize = [&](int c) { return nc - c > kMfG + 1 ? kMfG : nc - c; };
-        uint32_t ww = WIN ? mf_win_word(U + b0, ub, R, 0, gsize(0)) : 0u;
+        uint32_t ww = WIN ? mf_win_word(U + b0, ub, R, 0, gsize(0), U2 + b0, nu2 - b0) : 0u;
         for (; nc - c0 > kMfG + 1; c0 += kMfG) {
             if constexpr (WIN)
                 mf_group_win<kMfG>(ww, U + b0, ub, gsize(c0 + kMfG), &ww, RS, tab, VI, vlo, R, D, nv,
-                                   tlo, Te, c0, OUTs);
+                                   tlo, Te, c0, OUTs, U2 + b0, nu2 - b0);
             else mf_group<kMfG, !LEAN>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
         }
         switch (nc - c0) {
 #define HM_MF_TAIL(G) \
     case G:                                                                                      \
         if constexpr (WIN)                                                                       \
-            mf_group_win<G>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0, OUTs); \
+            mf_group_win<G>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0, OUTs,  \
+                            U2 + b0, nu2 - b0);                                                  \
         else mf_group<G, !LEAN>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);                     \
         break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
