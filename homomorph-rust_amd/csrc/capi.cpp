@@ -654,7 +654,10 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     E.top1 = c->pk_top1 ? 1u : 0u;
 #endif
     std::memcpy(E.topcol, c->pk_topcol, sizeof(E.topcol));
-    if (!masks && encrypt_fusable(E)) {
+#ifndef HM_ENC_FUSED
+#define HM_ENC_FUSED 1 // masks drawn inside the encryption kernel (A/B knob)
+#endif
+    if (!masks && HM_ENC_FUSED && encrypt_fusable(E)) {
         // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): the device
         // ChaCha20 stream, drawn inside the encryption kernel (the same keystream bytes a draw into
         // the mask buffer would hold, so the masks never round-trip HBM)
