@@ -273,18 +273,20 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin
     a += b, d = rotl32(d ^ a, 16), c += d, b = rotl32(b ^ c, 12), a += b, d = rotl32(d ^ a, 8),   \
     c += d, b = rotl32(b ^ c, 7)
 
-__device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint64_t blk, uint64_t nonce,
-                                               uint32_t (&x)[16]) {
-    uint32_t s[16];
+__device__ __forceinline__ void chacha20_init(const uint32_t (&key)[8], uint64_t blk, uint64_t nonce,
+                                              uint32_t (&s)[16]) {
     s[0] = 0x61707865u, s[1] = 0x3320646eu, s[2] = 0x79622d32u, s[3] = 0x6b206574u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[4 + i] = key[i];
     s[12] = (uint32_t)blk, s[13] = (uint32_t)(blk >> 32);
     s[14] = (uint32_t)nonce, s[15] = (uint32_t)(nonce >> 32);
+}
+
+// n double rounds (column + diagonal quarter rounds) of the ChaCha state x
+template <int N>
+__device__ __forceinline__ void chacha20_rounds(uint32_t (&x)[16]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = s[i];
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < N; ++r) {
         HM_QR(x[0], x[4], x[8], x[12]);
         HM_QR(x[1], x[5], x[9], x[13]);
         HM_QR(x[2], x[6], x[10], x[14]);
@@ -294,6 +296,15 @@ __device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint64_
         HM_QR(x[2], x[7], x[8], x[13]);
         HM_QR(x[3], x[4], x[9], x[14]);
     }
+}
+
+__device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint64_t blk, uint64_t nonce,
+                                               uint32_t (&x)[16]) {
+    uint32_t s[16];
+    chacha20_init(key, blk, nonce, s);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = s[i];
+    chacha20_rounds<10>(x);
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] += s[i];
 }
@@ -323,10 +334,11 @@ __global__ void __launch_bounds__(kEncBlock) encrypt_chacha_kernel(EncArgs E, Ra
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nonce = *R.nonce;
     const uint64_t wstep = (uint64_t)gridDim.x * (blockDim.x >> 6) * 256;
-    for (uint64_t T0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256;
-         T0 < total; T0 += wstep) {
-        uint32_t x[16];
-        chacha20_block(R.key, T0 / 4 + lane, nonce, x);
+    uint64_t T0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256;
+    if (T0 >= total) return; // whole wave
+    uint32_t x[16];
+    chacha20_block(R.key, T0 / 4 + lane, nonce, x);
+    for (; T0 < total; T0 += wstep) {
         uint4 *s4 = (uint4 *)st;
 #pragma unroll
         for (int i = 0; i < 4; ++i) s4[4 * lane + i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
@@ -335,12 +347,23 @@ __global__ void __launch_bounds__(kEncBlock) encrypt_chacha_kernel(EncArgs E, Ra
 #pragma unroll
         for (int i = 0; i < 4; ++i) mw[i] = s4[64 * i + lane]; // bit T0 + 64 i + lane
         wsync();
-#pragma unroll 1
+        // the next 256 bits' keystream block, its double rounds spread between this slice's four
+        // 64-bit encryptions (VALU work beside their LDS lookups; 3 + 2 + 3 + 2 double rounds)
+        uint32_t y[16];
+        chacha20_init(R.key, (T0 + wstep) / 4 + lane, nonce, y);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = y[i];
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint64_t t0 = T0 + 64 * i;
-            if (t0 >= total) break;
-            enc_bits_t128<PC, TOP1>(E, tab4, st, t0, total, nbits, mw[i]);
+            if (t0 < total) enc_bits_t128<PC, TOP1>(E, tab4, st, t0, total, nbits, mw[i]);
+            if (i % 2 == 0) chacha20_rounds<3>(x);
+            else chacha20_rounds<2>(x);
         }
+        // (the block's input words again: constants, key and nonce are wave-uniform)
+        chacha20_init(R.key, (T0 + wstep) / 4 + lane, nonce, y);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] += y[i];
     }
 }
 
