@@ -124,6 +124,7 @@ hm_status upload_pk(hm_ctx *c) {
     HM_HIP(c, hipStreamSynchronize(c->stream));
     retire(c, c->d_pk, 0, false), c->d_pk = nullptr;
     retire(c, c->d_pk_tab, 0, false), c->d_pk_tab = nullptr;
+    retire(c, c->d_pk_tab1, 0, false), c->d_pk_tab1 = nullptr;
     HM_HIP(c, hipMalloc(&c->d_pk, c->pk.size() * 8));
     HM_HIP(c, hipMemcpy(c->d_pk, c->pk.data(), c->pk.size() * 8, hipMemcpyHostToDevice));
     const uint32_t G = (c->pk_tau + 3) / 4, PC = c->pk_cap, NP = (PC + 1) / 2;
@@ -139,6 +140,19 @@ hm_status upload_pk(hm_ctx *c) {
                                 c->pk[(size_t)(4 * grp + k) * PC + l];
         HM_HIP(c, hipMalloc(&c->d_pk_tab, words * 8));
         HM_HIP(c, hipMemcpy(c->d_pk_tab, tab.data(), words * 8, hipMemcpyHostToDevice));
+        if (c->pk_top1) {
+            // the same table without the one-bit top limb (EncArgs::top1): pairs of limbs
+            // 0 .. PC-2 only, NP1 = (PC - 1 + 1) / 2 pairs per group -- a third smaller at PC = 5
+            const uint32_t NP1 = PC / 2;
+            std::vector<uint64_t> tab1((size_t)G * NP1 * 32, 0);
+            for (uint32_t grp = 0; grp < G; ++grp)
+                for (uint32_t p = 0; p < NP1; ++p)
+                    for (uint32_t k = 0; k < 32; ++k)
+                        if (2 * p + k % 2 < PC - 1)
+                            tab1[((size_t)grp * NP1 + p) * 32 + k] = tab[((size_t)grp * NP + p) * 32 + k];
+            HM_HIP(c, hipMalloc(&c->d_pk_tab1, tab1.size() * 8));
+            HM_HIP(c, hipMemcpy(c->d_pk_tab1, tab1.data(), tab1.size() * 8, hipMemcpyHostToDevice));
+        }
     }
     return HM_OK;
 }
@@ -283,8 +297,11 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_status, sizeof(int));
     if (e == hipSuccess) e = hipMemset(c->d_status, 0, sizeof(int));
-    if (e == hipSuccess) e = hipMalloc(&c->d_nonce, sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMemcpy(c->d_nonce, &nonce0, sizeof(uint64_t), hipMemcpyHostToDevice);
+    // [0] the ChaCha20 nonce, [1] the fused encryption's finished-block counter (zero between
+    // launches: its last block resets it and advances the nonce)
+    const uint64_t nonce_init[2] = {nonce0, 0};
+    if (e == hipSuccess) e = hipMalloc(&c->d_nonce, sizeof(nonce_init));
+    if (e == hipSuccess) e = hipMemcpy(c->d_nonce, nonce_init, sizeof(nonce_init), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         if (c->d_status) (void)hipFree(c->d_status);
         if (c->d_nonce) (void)hipFree(c->d_nonce);
@@ -317,7 +334,7 @@ void hm_ctx_destroy(hm_ctx *c) try {
     drop_secret(c);
     if (c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
     mul_plans_release(c);
-    for (void *p : {(void *)c->d_pk, (void *)c->d_pk_tab, (void *)c->d_s,
+    for (void *p : {(void *)c->d_pk, (void *)c->d_pk_tab, (void *)c->d_pk_tab1, (void *)c->d_s,
                     (void *)c->d_ws_add, (void *)c->d_status, (void *)c->d_nonce,
                     (void *)c->d_masks, (void *)c->d_mws})
         if (p) (void)hipFree(p);
@@ -636,6 +653,7 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     EncArgs E{};
     E.pk = c->d_pk, E.tau = c->pk_tau, E.pk_cap = c->pk_cap;
     E.pk_tab = c->d_pk_tab;
+    E.pk_tab1 = c->d_pk_tab1;
     E.cus = c->cus;
     E.lognbits = -1;
     for (int s = 0; s < 8; ++s)
@@ -651,7 +669,7 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
         E.uniform_cap &= cap_of(out->bound[i]) == c->pk_cap;
     }
 #ifndef HM_ENC_NO_TOP1
-    E.top1 = c->pk_top1 ? 1u : 0u;
+    E.top1 = c->pk_top1 && c->d_pk_tab1 ? 1u : 0u;
 #endif
     std::memcpy(E.topcol, c->pk_topcol, sizeof(E.topcol));
 #ifndef HM_ENC_FUSED

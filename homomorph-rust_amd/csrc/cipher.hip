@@ -112,6 +112,9 @@ __device__ __forceinline__ void enc_lookup2(uint32_t *acc, const uint4 *tab4, ui
 #ifndef HM_ENC_NT
 #define HM_ENC_NT 0 // non-temporal ciphertext stores (A/B knob)
 #endif
+#ifndef HM_ENC_LDS_DEPTH
+#define HM_ENC_LDS_DEPTH 0 // (A/B knob) lookups per read batch in enc_bits_t128; 0: compiler's
+#endif
 // The wave's 64 ciphertext bits t0 .. t0 + 63 once their subset sums are in acc: the plaintext
 // bit, the degree, and the stores (uniform caps: the wave's 64 * PC consecutive output limbs,
 // transposed through its LDS stage and stored coalesced; otherwise per bit at its offset)
@@ -167,11 +170,14 @@ __device__ __forceinline__ void enc_finish(const EncArgs &E, uint64_t *acc, uint
 // row i's bit 64 (PC - 1): five VALU instead of 32 table reads of 8 B and 32 XORs per ciphertext
 // bit (a fifth of the LDS traffic at PC = 5).
 template <int PC, bool TOP1>
+constexpr int kEncTabPairs = ((TOP1 ? PC - 1 : PC) + 1) / 2; // limb pairs per group of the table read
+
+template <int PC, bool TOP1>
 __device__ __forceinline__ void enc_bits_t128(const EncArgs &E, const uint4 *tab4, uint64_t *st,
                                               uint64_t t0, uint64_t total, uint32_t nbits,
                                               const uint4 &mw) {
-    constexpr int NP = (PC + 1) / 2;       // the table's limb pairs per group
-    constexpr int PL = TOP1 ? PC - 1 : PC; // limbs looked up
+    constexpr int PL = TOP1 ? PC - 1 : PC;      // limbs looked up (TOP1: E.pk_tab1, without the top)
+    constexpr int NP = kEncTabPairs<PC, TOP1>; // the table's limb pairs per group
     const uint32_t lane = threadIdx.x & 63u;
     const bool live = t0 + lane < total;
     const uint64_t t = live ? t0 + lane : total - 1;
@@ -184,8 +190,13 @@ __device__ __forceinline__ void enc_bits_t128(const EncArgs &E, const uint4 *tab
 #pragma unroll
     for (int w = 0; w < 4; ++w)
 #pragma unroll
-        for (int j = 0; j < 8; j += 2)
+        for (int j = 0; j < 8; j += 2) {
             enc_lookup2<PL, NP>(a32, tab4, 8 * w + j, (ws[w] >> (4 * j)) & 15u, (ws[w] >> (4 * j + 4)) & 15u);
+#if HM_ENC_LDS_DEPTH
+            // (knob) keep the reads of the next lookups below this point
+            if (j % (2 * HM_ENC_LDS_DEPTH) == 2 * HM_ENC_LDS_DEPTH - 2) asm volatile("" ::: "memory");
+#endif
+        }
     if constexpr (TOP1) {
         const uint32_t x = (mw.x & E.topcol[0]) ^ (mw.y & E.topcol[1]) ^ (mw.z & E.topcol[2]) ^
                            (mw.w & E.topcol[3]);
@@ -197,12 +208,11 @@ __device__ __forceinline__ void enc_bits_t128(const EncArgs &E, const uint4 *tab
     enc_finish<PC>(E, acc, st, t0, total, live, e, k, nbits);
 }
 
-// Copies the key's nibble table (G groups) into the block's LDS
-template <int PC>
-__device__ __forceinline__ void enc_table_to_lds(const EncArgs &E, uint32_t G, uint64_t *tab) {
-    constexpr int NP = (PC + 1) / 2;
+// Copies a nibble table (G groups of NP limb pairs) into the block's LDS
+template <int NP>
+__device__ __forceinline__ void enc_table_to_lds(const uint64_t *ptab, uint32_t G, uint64_t *tab) {
     const uint32_t n16 = G * NP * 16; // 16-byte chunks
-    const uint4 *src = (const uint4 *)E.pk_tab;
+    const uint4 *src = (const uint4 *)ptab;
     uint4 *dst = (uint4 *)tab;
     for (uint32_t f = threadIdx.x; f < n16; f += blockDim.x) dst[f] = src[f];
     __syncthreads();
@@ -210,12 +220,16 @@ __device__ __forceinline__ void enc_table_to_lds(const EncArgs &E, uint32_t G, u
 
 // GC: compile-time group count (tau/4) for the fully unrolled path with 16-byte-aligned masks
 // (tau = 128: one uint4 of mask per ciphertext bit, read one iteration ahead), 0 = any tau
+#ifndef HM_ENC_TAB_WPE
+#define HM_ENC_TAB_WPE 7 // (A/B knob) waves per SIMD of the table kernel
+#endif
 template <int PC, int GC, bool TOP1 = false>
-__global__ void __launch_bounds__(kEncBlock) encrypt_table_kernel(EncArgs E) {
-    constexpr int NP = (PC + 1) / 2;  // limb pairs
-    extern __shared__ uint64_t tab[]; // [G][NP][16][2] (upload_pk)
+__global__ void __launch_bounds__(kEncBlock) __attribute__((amdgpu_waves_per_eu(HM_ENC_TAB_WPE)))
+encrypt_table_kernel(EncArgs E) {
+    constexpr int NP = kEncTabPairs<PC, TOP1>; // limb pairs (TOP1: the table without the top limb)
+    extern __shared__ uint64_t tab[];          // [G][NP][16][2] (upload_pk)
     const uint32_t G = GC ? GC : (E.tau + 3) / 4;
-    enc_table_to_lds<PC>(E, G, tab);
+    enc_table_to_lds<NP>(TOP1 ? E.pk_tab1 : E.pk_tab, G, tab);
     const uint4 *tab4 = (const uint4 *)tab;
     uint64_t *stage = tab + (size_t)G * NP * 32; // [waves][64][PC] store transpose
     uint64_t *st = stage + (size_t)(threadIdx.x & ~63u) * PC;
@@ -320,13 +334,17 @@ __device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint64_
 // memory; rand_bump_kernel advances it after the launch, as after a draw.
 __global__ void rand_bump_kernel(uint64_t *nonce);
 
+#ifndef HM_ENC_CHA_WPE
+#define HM_ENC_CHA_WPE 6 // waves per SIMD: 3 blocks of 8 waves per CU (LDS 48 KB each at PC = 5)
+#endif
 template <int PC, bool TOP1>
-__global__ void __launch_bounds__(kEncBlock) encrypt_chacha_kernel(EncArgs E, RandArgs R) {
-    constexpr int NP = (PC + 1) / 2;
+__global__ void __launch_bounds__(kEncBlock) __attribute__((amdgpu_waves_per_eu(HM_ENC_CHA_WPE)))
+encrypt_chacha_kernel(EncArgs E, RandArgs R) {
+    constexpr int NP = kEncTabPairs<PC, TOP1>;
     constexpr uint32_t kStageWords = 64 * PC > 512 ? 64 * PC : 512; // u64: 64 lanes x 64 B of keystream
     extern __shared__ uint64_t tab[];
     constexpr uint32_t G = 32;
-    enc_table_to_lds<PC>(E, G, tab);
+    enc_table_to_lds<NP>(TOP1 ? E.pk_tab1 : E.pk_tab, G, tab);
     const uint4 *tab4 = (const uint4 *)tab;
     uint64_t *st = tab + (size_t)G * NP * 32 + (size_t)(threadIdx.x >> 6) * kStageWords;
     const uint32_t nbits = E.nbytes * 8;
@@ -335,9 +353,8 @@ __global__ void __launch_bounds__(kEncBlock) encrypt_chacha_kernel(EncArgs E, Ra
     const uint64_t nonce = *R.nonce;
     const uint64_t wstep = (uint64_t)gridDim.x * (blockDim.x >> 6) * 256;
     uint64_t T0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256;
-    if (T0 >= total) return; // whole wave
     uint32_t x[16];
-    chacha20_block(R.key, T0 / 4 + lane, nonce, x);
+    if (T0 < total) chacha20_block(R.key, T0 / 4 + lane, nonce, x);
     for (; T0 < total; T0 += wstep) {
         uint4 *s4 = (uint4 *)st;
 #pragma unroll
@@ -365,14 +382,27 @@ __global__ void __launch_bounds__(kEncBlock) encrypt_chacha_kernel(EncArgs E, Ra
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] += y[i];
     }
+    // the draw consumed this nonce's keystream: the last block to finish (every block read the
+    // nonce when it started) advances it and resets the counter, so no separate bump launch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned long long done = atomicAdd((unsigned long long *)&R.nonce[1], 1ull);
+        if (done + 1 == (unsigned long long)gridDim.x) {
+            atomicExch((unsigned long long *)&R.nonce[1], 0ull);
+            atomicAdd((unsigned long long *)&R.nonce[0], 1ull);
+        }
+    }
 }
 
 template <int PC>
 static void launch_enc_pc(const EncArgs &E, const RandArgs *R, void *stream) {
     const uint64_t threads = E.n * E.nbytes * 8;
     const size_t tab = (size_t)((E.tau + 3) / 4) * ((PC + 1) / 2) * 16 * 16;
+    const size_t tab1 = (size_t)((E.tau + 3) / 4) * (PC / 2) * 16 * 16; // (top1: without the top limb)
     if (R) { // fused draw (the host checked tau == 128 and the table)
-        const size_t lds = tab + (size_t)(kEncBlock / 64) * 8 * (64 * PC > 512 ? 64 * PC : 512);
+        const size_t lds = (E.top1 && PC > 1 ? tab1 : tab) +
+                           (size_t)(kEncBlock / 64) * 8 * (64 * PC > 512 ? 64 * PC : 512);
         const uint64_t want = ((threads + 255) / 256 + kEncBlock / 64 - 1) / (kEncBlock / 64);
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
         const uint64_t blocks = std::min<uint64_t>(want, (uint64_t)E.cus * per_cu);
@@ -384,13 +414,14 @@ static void launch_enc_pc(const EncArgs &E, const RandArgs *R, void *stream) {
                                lds, (hipStream_t)stream, E, *R);
         return;
     }
-    const size_t lds = tab + (size_t)kEncBlock * PC * 8; // + the store transpose
+    const bool t1 = E.tau == 128 && ((uintptr_t)E.masks & 15u) == 0 && E.top1 && PC > 1;
+    const size_t lds = (t1 ? tab1 : tab) + (size_t)kEncBlock * PC * 8; // + the store transpose
     if (E.pk_tab && tab <= kEncTableBytes && lds <= 160 * 1024) { // one CU's LDS at most
         // a few resident blocks per CU, each striding over bits (the table copy is amortised)
         const uint64_t want = (threads + kEncBlock - 1) / kEncBlock;
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
         const uint64_t blocks = std::min<uint64_t>(want, (uint64_t)E.cus * per_cu);
-        if (E.tau == 128 && ((uintptr_t)E.masks & 15u) == 0 && E.top1 && PC > 1)
+        if (t1)
             hipLaunchKernelGGL((encrypt_table_kernel<PC, 32, (PC > 1)>), dim3((unsigned)blocks),
                                dim3(kEncBlock), lds, (hipStream_t)stream, E);
         else if (E.tau == 128 && ((uintptr_t)E.masks & 15u) == 0)
@@ -435,12 +466,7 @@ int launch_encrypt(const EncArgs &E, const RandArgs *R, void *stream) {
     case 17: launch_enc_pc<17>(E, R, stream); break;
     default: return HM_ERR_UNSUPPORTED;
     }
-    if (hipGetLastError() != hipSuccess) return -1;
-    if (R) { // the draw consumed this nonce's keystream
-        hipLaunchKernelGGL(rand_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, R->nonce);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    return 0;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -38,6 +38,7 @@ struct hm_ctx {
     // device state
     uint64_t *d_pk = nullptr;
     uint64_t *d_pk_tab = nullptr;      // encryption nibble table (upload_pk), or null
+    uint64_t *d_pk_tab1 = nullptr;     // the same without the one-bit top limb (pk_top1), or null
     uint64_t *d_z = nullptr;           // decrypt parity table z_k = (X^k mod S)(0)
     uint32_t z_limbs = 0;
     uint64_t *d_s = nullptr;           // divisor scratch for hm_poly_rem_batch

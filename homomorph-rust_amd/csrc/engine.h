@@ -50,6 +50,7 @@ struct AddArgs {
 struct EncArgs {
     const uint64_t *pk;     // tau * pk_cap limbs
     const uint64_t *pk_tab; // nibble table [ceil(tau/4)][limb pair][16][2] (upload_pk), or null
+    const uint64_t *pk_tab1; // the same over limbs 0 .. pk_cap - 2 (top1 keys), or null
     uint32_t cus;           // compute units (grid sizing)
     uint32_t tau, pk_cap;
     const uint8_t *data;
@@ -289,7 +290,7 @@ struct PolyArgs {
 // *nonce and advanced by one per draw).  Block b of the draw fills bytes [64b, 64b + 64).
 struct RandArgs {
     uint32_t key[8];
-    uint64_t *nonce;
+    uint64_t *nonce; // [0] nonce, [1] finished-block counter of the fused encryption
     uint8_t *out;
     uint64_t nbytes;
 };
