@@ -3,7 +3,7 @@ shape (context.rs:555-595 examples), captured-graph validity across buffer chang
 import numpy as np
 import pytest
 
-from helpers import as_bytes, assert_batches_equal, masks, plain, seeded_value_masks
+from helpers import as_bytes, assert_batches_equal, masks, plain, seeded_random_bytes, seeded_value_masks
 
 pytestmark = pytest.mark.gpu
 
