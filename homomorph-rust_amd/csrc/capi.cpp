@@ -210,12 +210,12 @@ hm_status ensure_ztable(hm_ctx *c, uint32_t max_bound) {
 // n bytes of the context's ChaCha20 keystream into device memory: the kernel reads the nonce
 // from device memory and a second launch advances it, so every draw -- also every replay of a
 // captured graph that contains one -- uses a fresh keystream (DESIGN.md "Randomness").
-hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n) {
+hm_status draw_random(hm_ctx *c, uint8_t *dst, size_t n, bool bump = true) {
     if (!n) return HM_OK;
     RandArgs R{};
     std::memcpy(R.key, c->chacha_key, sizeof(R.key));
     R.nonce = c->d_nonce, R.out = dst, R.nbytes = n;
-    const int r = launch_random(R, c->stream);
+    const int r = launch_random(R, c->stream, bump);
     wipe(R.key, sizeof(R.key));
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
 }
@@ -297,11 +297,8 @@ hm_status hm_ctx_create(uint16_t d, uint16_t dp, uint16_t delta, uint16_t tau, i
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_status, sizeof(int));
     if (e == hipSuccess) e = hipMemset(c->d_status, 0, sizeof(int));
-    // [0] the ChaCha20 nonce, [1] the fused encryption's finished-block counter (zero between
-    // launches: its last block resets it and advances the nonce)
-    const uint64_t nonce_init[2] = {nonce0, 0};
-    if (e == hipSuccess) e = hipMalloc(&c->d_nonce, sizeof(nonce_init));
-    if (e == hipSuccess) e = hipMemcpy(c->d_nonce, nonce_init, sizeof(nonce_init), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&c->d_nonce, sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMemcpy(c->d_nonce, &nonce0, sizeof(uint64_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         if (c->d_status) (void)hipFree(c->d_status);
         if (c->d_nonce) (void)hipFree(c->d_nonce);
@@ -672,32 +669,20 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     E.top1 = c->pk_top1 && c->d_pk_tab1 ? 1u : 0u;
 #endif
     std::memcpy(E.topcol, c->pk_topcol, sizeof(E.topcol));
-#ifndef HM_ENC_FUSED
-#define HM_ENC_FUSED 1 // masks drawn inside the encryption kernel (A/B knob)
-#endif
-    if (!masks && HM_ENC_FUSED && encrypt_fusable(E)) {
-        // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): the device
-        // ChaCha20 stream, drawn inside the encryption kernel (the same keystream bytes a draw into
-        // the mask buffer would hold, so the masks never round-trip HBM)
-        RandArgs R{};
-        std::memcpy(R.key, c->chacha_key, sizeof(R.key));
-        R.nonce = c->d_nonce;
-        const int r = launch_encrypt(E, &R, c->stream);
-        wipe(R.key, sizeof(R.key));
-        if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
-        return r ? hip_fail(c, hipGetLastError()) : HM_OK;
-    }
     if (!masks) {
-        // otherwise the stream is drawn into the context's mask buffer right before the launch
+        // CipheredBit::part draws ceil(tau/8) random bytes per bit (cipher.rs:92-97): here the
+        // device ChaCha20 stream, drawn into the context's mask buffer right before the launch;
+        // the encryption kernel advances the nonce (no bump launch of its own)
         const size_t mb = (size_t)out->n * out->nbits * ((c->pk_tau + 7) / 8);
         const size_t need = (mb + 63) & ~(size_t)63;
         if (need > c->masks_bytes && c->d_masks) (void)hipMemset(c->d_masks, 0, c->masks_bytes);
         HM_HIP(c, grow(c, c->d_masks, c->masks_bytes, need));
-        if (hm_status st = draw_random(c, c->d_masks, mb); st) return st;
+        if (hm_status st = draw_random(c, c->d_masks, mb, false); st) return st;
         masks = c->d_masks;
+        E.nonce_bump = c->d_nonce;
     }
     E.masks = masks;
-    int r = launch_encrypt(E, nullptr, c->stream);
+    int r = launch_encrypt(E, c->stream);
     if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
 } HM_ABI_CATCH

@@ -16,8 +16,15 @@ namespace hm {
 // (CipheredBit::cipher, cipher.rs:99-115; Ciphered::try_cipher bit order :180-185).  The public
 // key T_i is read with wave-uniform addresses (scalar loads); the mask select is one bitop3
 // (acc ^ (t & m)) per 32-bit half.
+// The draw that made this launch's masks left its nonce for the encryption to advance (one plain
+// store by one thread: nothing in the encryption reads the nonce), saving a launch per encrypt
+__device__ __forceinline__ void enc_nonce_bump(const EncArgs &E) {
+    if (E.nonce_bump && blockIdx.x == 0 && threadIdx.x == 0) *E.nonce_bump += 1;
+}
+
 template <int PC>
 __global__ void __launch_bounds__(256) encrypt_kernel(EncArgs E) {
+    enc_nonce_bump(E);
     const uint32_t nbits = E.nbytes * 8;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= E.n * nbits) return;
@@ -226,6 +233,7 @@ __device__ __forceinline__ void enc_table_to_lds(const uint64_t *ptab, uint32_t 
 template <int PC, int GC, bool TOP1 = false>
 __global__ void __launch_bounds__(kEncBlock) __attribute__((amdgpu_waves_per_eu(HM_ENC_TAB_WPE)))
 encrypt_table_kernel(EncArgs E) {
+    enc_nonce_bump(E);
     constexpr int NP = kEncTabPairs<PC, TOP1>; // limb pairs (TOP1: the table without the top limb)
     extern __shared__ uint64_t tab[];          // [G][NP][16][2] (upload_pk)
     const uint32_t G = GC ? GC : (E.tau + 3) / 4;
@@ -324,96 +332,11 @@ __device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint64_
 }
 #undef HM_QR
 
-// Encryption with the masks drawn inside the kernel (hm_encrypt_batch without caller masks,
-// tau = 128): the mask of ciphertext bit t is keystream bytes 16 t .. 16 t + 15 -- exactly the
-// bytes rand_fill_kernel would have written to the mask buffer -- so a wave takes 256 bits at a
-// time: lane L computes keystream block T0/4 + L (the masks of bits T0 + 4L .. T0 + 4L + 3), the
-// blocks meet in the wave's LDS stage, each lane reads back the masks of its bits T0 + 64 i + L
-// (i = 0..3), and the four 64-bit slices run as in encrypt_table_kernel.  The masks never touch
-// HBM (512 B per u32 written and read back by the unfused path).  The nonce is read from device
-// memory; rand_bump_kernel advances it after the launch, as after a draw.
-__global__ void rand_bump_kernel(uint64_t *nonce);
-
-#ifndef HM_ENC_CHA_WPE
-#define HM_ENC_CHA_WPE 6 // waves per SIMD: 3 blocks of 8 waves per CU (LDS 48 KB each at PC = 5)
-#endif
-template <int PC, bool TOP1>
-__global__ void __launch_bounds__(kEncBlock) __attribute__((amdgpu_waves_per_eu(HM_ENC_CHA_WPE)))
-encrypt_chacha_kernel(EncArgs E, RandArgs R) {
-    constexpr int NP = kEncTabPairs<PC, TOP1>;
-    constexpr uint32_t kStageWords = 64 * PC > 512 ? 64 * PC : 512; // u64: 64 lanes x 64 B of keystream
-    extern __shared__ uint64_t tab[];
-    constexpr uint32_t G = 32;
-    enc_table_to_lds<NP>(TOP1 ? E.pk_tab1 : E.pk_tab, G, tab);
-    const uint4 *tab4 = (const uint4 *)tab;
-    uint64_t *st = tab + (size_t)G * NP * 32 + (size_t)(threadIdx.x >> 6) * kStageWords;
-    const uint32_t nbits = E.nbytes * 8;
-    const uint64_t total = E.n * nbits;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t nonce = *R.nonce;
-    const uint64_t wstep = (uint64_t)gridDim.x * (blockDim.x >> 6) * 256;
-    uint64_t T0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256;
-    uint32_t x[16];
-    if (T0 < total) chacha20_block(R.key, T0 / 4 + lane, nonce, x);
-    for (; T0 < total; T0 += wstep) {
-        uint4 *s4 = (uint4 *)st;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s4[4 * lane + i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
-        wsync();
-        uint4 mw[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mw[i] = s4[64 * i + lane]; // bit T0 + 64 i + lane
-        wsync();
-        // the next 256 bits' keystream block, its double rounds spread between this slice's four
-        // 64-bit encryptions (VALU work beside their LDS lookups; 3 + 2 + 3 + 2 double rounds)
-        uint32_t y[16];
-        chacha20_init(R.key, (T0 + wstep) / 4 + lane, nonce, y);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = y[i];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint64_t t0 = T0 + 64 * i;
-            if (t0 < total) enc_bits_t128<PC, TOP1>(E, tab4, st, t0, total, nbits, mw[i]);
-            if (i % 2 == 0) chacha20_rounds<3>(x);
-            else chacha20_rounds<2>(x);
-        }
-        // (the block's input words again: constants, key and nonce are wave-uniform)
-        chacha20_init(R.key, (T0 + wstep) / 4 + lane, nonce, y);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] += y[i];
-    }
-    // the draw consumed this nonce's keystream: the last block to finish (every block read the
-    // nonce when it started) advances it and resets the counter, so no separate bump launch
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned long long done = atomicAdd((unsigned long long *)&R.nonce[1], 1ull);
-        if (done + 1 == (unsigned long long)gridDim.x) {
-            atomicExch((unsigned long long *)&R.nonce[1], 0ull);
-            atomicAdd((unsigned long long *)&R.nonce[0], 1ull);
-        }
-    }
-}
-
 template <int PC>
-static void launch_enc_pc(const EncArgs &E, const RandArgs *R, void *stream) {
+static void launch_enc_pc(const EncArgs &E, void *stream) {
     const uint64_t threads = E.n * E.nbytes * 8;
     const size_t tab = (size_t)((E.tau + 3) / 4) * ((PC + 1) / 2) * 16 * 16;
     const size_t tab1 = (size_t)((E.tau + 3) / 4) * (PC / 2) * 16 * 16; // (top1: without the top limb)
-    if (R) { // fused draw (the host checked tau == 128 and the table)
-        const size_t lds = (E.top1 && PC > 1 ? tab1 : tab) +
-                           (size_t)(kEncBlock / 64) * 8 * (64 * PC > 512 ? 64 * PC : 512);
-        const uint64_t want = ((threads + 255) / 256 + kEncBlock / 64 - 1) / (kEncBlock / 64);
-        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(4, (160 * 1024) / lds));
-        const uint64_t blocks = std::min<uint64_t>(want, (uint64_t)E.cus * per_cu);
-        if (E.top1 && PC > 1)
-            hipLaunchKernelGGL((encrypt_chacha_kernel<PC, (PC > 1)>), dim3((unsigned)blocks), dim3(kEncBlock),
-                               lds, (hipStream_t)stream, E, *R);
-        else
-            hipLaunchKernelGGL((encrypt_chacha_kernel<PC, false>), dim3((unsigned)blocks), dim3(kEncBlock),
-                               lds, (hipStream_t)stream, E, *R);
-        return;
-    }
     const bool t1 = E.tau == 128 && ((uintptr_t)E.masks & 15u) == 0 && E.top1 && PC > 1;
     const size_t lds = (t1 ? tab1 : tab) + (size_t)kEncBlock * PC * 8; // + the store transpose
     if (E.pk_tab && tab <= kEncTableBytes && lds <= 160 * 1024) { // one CU's LDS at most
@@ -437,33 +360,26 @@ static void launch_enc_pc(const EncArgs &E, const RandArgs *R, void *stream) {
                        (hipStream_t)stream, E);
 }
 
-bool encrypt_fusable(const EncArgs &E) {
-    return E.tau == 128 && E.pk_tab && E.pk_cap >= 1 && E.pk_cap <= 17 &&
-           (size_t)32 * ((E.pk_cap + 1) / 2) * 256 + (size_t)(kEncBlock / 64) * 8 *
-                   (64 * E.pk_cap > 512 ? 64 * E.pk_cap : 512) <= 160 * 1024;
-}
-
-int launch_encrypt(const EncArgs &E, const RandArgs *R, void *stream) {
+int launch_encrypt(const EncArgs &E, void *stream) {
     if (E.n == 0) return 0;
-    if (R && !encrypt_fusable(E)) return HM_ERR_UNSUPPORTED;
     switch (E.pk_cap) {
-    case 1: launch_enc_pc<1>(E, R, stream); break;
-    case 2: launch_enc_pc<2>(E, R, stream); break;
-    case 3: launch_enc_pc<3>(E, R, stream); break;
-    case 4: launch_enc_pc<4>(E, R, stream); break;
-    case 5: launch_enc_pc<5>(E, R, stream); break;
-    case 6: launch_enc_pc<6>(E, R, stream); break;
-    case 7: launch_enc_pc<7>(E, R, stream); break;
-    case 8: launch_enc_pc<8>(E, R, stream); break;
-    case 9: launch_enc_pc<9>(E, R, stream); break;
-    case 10: launch_enc_pc<10>(E, R, stream); break;
-    case 11: launch_enc_pc<11>(E, R, stream); break;
-    case 12: launch_enc_pc<12>(E, R, stream); break;
-    case 13: launch_enc_pc<13>(E, R, stream); break;
-    case 14: launch_enc_pc<14>(E, R, stream); break;
-    case 15: launch_enc_pc<15>(E, R, stream); break;
-    case 16: launch_enc_pc<16>(E, R, stream); break;
-    case 17: launch_enc_pc<17>(E, R, stream); break;
+    case 1: launch_enc_pc<1>(E, stream); break;
+    case 2: launch_enc_pc<2>(E, stream); break;
+    case 3: launch_enc_pc<3>(E, stream); break;
+    case 4: launch_enc_pc<4>(E, stream); break;
+    case 5: launch_enc_pc<5>(E, stream); break;
+    case 6: launch_enc_pc<6>(E, stream); break;
+    case 7: launch_enc_pc<7>(E, stream); break;
+    case 8: launch_enc_pc<8>(E, stream); break;
+    case 9: launch_enc_pc<9>(E, stream); break;
+    case 10: launch_enc_pc<10>(E, stream); break;
+    case 11: launch_enc_pc<11>(E, stream); break;
+    case 12: launch_enc_pc<12>(E, stream); break;
+    case 13: launch_enc_pc<13>(E, stream); break;
+    case 14: launch_enc_pc<14>(E, stream); break;
+    case 15: launch_enc_pc<15>(E, stream); break;
+    case 16: launch_enc_pc<16>(E, stream); break;
+    case 17: launch_enc_pc<17>(E, stream); break;
     default: return HM_ERR_UNSUPPORTED;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -592,19 +508,40 @@ int launch_decrypt(const DecArgs &D, void *stream) {
 // Device CSPRNG for encryption masks: ChaCha20 (chacha20_block above), one 64-byte block per
 // thread.  The nonce is read from device memory and advanced by rand_bump_kernel after the draw,
 // so a graph replay never repeats a keystream.
+#ifndef HM_RAND_BLOCKS
+#define HM_RAND_BLOCKS 1 // keystream blocks per thread, computed together (A/B knob: ILP)
+#endif
+constexpr int kRandBlocks = HM_RAND_BLOCKS;
 __global__ void __launch_bounds__(256) rand_fill_kernel(RandArgs R) {
-    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blk * 64 >= R.nbytes) return;
-    uint32_t x[16];
-    chacha20_block(R.key, blk, *R.nonce, x);
-    uint8_t *dst = R.out + blk * 64;
-    if (blk * 64 + 64 <= R.nbytes && ((uintptr_t)dst & 15u) == 0) {
-        uint4 *d4 = (uint4 *)dst;
+    const uint64_t b0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRandBlocks;
+    if (b0 * 64 >= R.nbytes) return;
+    const uint64_t nonce = *R.nonce;
+    uint32_t s[kRandBlocks][16], x[kRandBlocks][16];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) d4[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
-    } else {
-        for (uint64_t k = 0; k < 64 && blk * 64 + k < R.nbytes; ++k)
-            dst[k] = (uint8_t)(x[k / 4] >> (8 * (k % 4)));
+    for (int q = 0; q < kRandBlocks; ++q) {
+        chacha20_init(R.key, b0 + q, nonce, s[q]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[q][i] = s[q][i];
+    }
+#pragma unroll
+    for (int r = 0; r < 10; ++r)
+#pragma unroll
+        for (int q = 0; q < kRandBlocks; ++q) chacha20_rounds<1>(x[q]);
+#pragma unroll
+    for (int q = 0; q < kRandBlocks; ++q) {
+        const uint64_t blk = b0 + q;
+        if (blk * 64 >= R.nbytes) break;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[q][i] += s[q][i];
+        uint8_t *dst = R.out + blk * 64;
+        if (blk * 64 + 64 <= R.nbytes && ((uintptr_t)dst & 15u) == 0) {
+            uint4 *d4 = (uint4 *)dst;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d4[i] = make_uint4(x[q][4 * i], x[q][4 * i + 1], x[q][4 * i + 2], x[q][4 * i + 3]);
+        } else {
+            for (uint64_t k = 0; k < 64 && blk * 64 + k < R.nbytes; ++k)
+                dst[k] = (uint8_t)(x[q][k / 4] >> (8 * (k % 4)));
+        }
     }
 }
 
@@ -612,11 +549,12 @@ __global__ void rand_bump_kernel(uint64_t *nonce) {
     if (threadIdx.x == 0) atomicAdd((unsigned long long *)nonce, 1ull);
 }
 
-int launch_random(const RandArgs &R, void *stream) {
+int launch_random(const RandArgs &R, void *stream, bool bump) {
     if (!R.nbytes) return 0;
-    const uint64_t blocks = (R.nbytes + 64 * 256 - 1) / (64 * 256);
+    const uint64_t blocks = (R.nbytes + 64 * 256 * kRandBlocks - 1) / (64 * 256 * kRandBlocks);
     hipLaunchKernelGGL(rand_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, R);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (!bump) return 0; // the caller's next launch advances the nonce (EncArgs::nonce_bump)
     hipLaunchKernelGGL(rand_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, R.nonce);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -67,6 +67,7 @@ struct EncArgs {
     // parity(mask & topcol), topcol bit i = row i's bit 64 (pk_cap - 1) (cipher.hip enc_bits_t128)
     uint32_t top1;
     uint32_t topcol[4];
+    uint64_t *nonce_bump; // non-null: advance this CSPRNG nonce (the masks were just drawn)
 };
 
 struct DecArgs {
@@ -290,13 +291,14 @@ struct PolyArgs {
 // *nonce and advanced by one per draw).  Block b of the draw fills bytes [64b, 64b + 64).
 struct RandArgs {
     uint32_t key[8];
-    uint64_t *nonce; // [0] nonce, [1] finished-block counter of the fused encryption
+    uint64_t *nonce;
     uint8_t *out;
     uint64_t nbytes;
 };
 
 // host-side launchers (kernels.hip)
-int launch_random(const RandArgs &a, void *stream);
+// bump false: the nonce is left for the caller's next launch to advance (EncArgs::nonce_bump)
+int launch_random(const RandArgs &a, void *stream, bool bump = true);
 // ev0/ev1 (hipEvent_t, may be null): recorded on the stream around the carry-chain launch
 int launch_add(const AddArgs &a, void *stream, void *ev0 = nullptr, void *ev1 = nullptr);
 int launch_add_prep(const AddArgs &a, void *stream);
@@ -304,10 +306,7 @@ int launch_add_prep(const AddArgs &a, void *stream);
 AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n);
 int launch_add_chain_mfma(const AddArgs &a, void *stream);
 int launch_add_chain_valu(const AddArgs &a, void *stream);
-// R: draw the masks inside the kernel from R's ChaCha20 stream (masks == null; tau = 128 only,
-// encrypt_fusable) and advance R's nonce, instead of reading a.masks
-int launch_encrypt(const EncArgs &a, const RandArgs *R, void *stream);
-bool encrypt_fusable(const EncArgs &a);
+int launch_encrypt(const EncArgs &a, void *stream);
 int launch_decrypt(const DecArgs &a, void *stream);
 int launch_gate(const GateArgs &a, void *stream);
 int launch_mul_stage(const MulStageArgs &a, void *stream);
