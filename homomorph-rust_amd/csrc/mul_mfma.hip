@@ -91,6 +91,44 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
     }
 }
 
+// One tile at a time with accumulators that keep counting across all of a wave's (tile, group)
+// sweeps (HM_MF_CONT): a sweep's parities are bit 0 of the accumulators now XOR bit 0 before it
+// (as the adder's chain does across tiles), so no 16 accumulator moves to 2^23 per tile -- a narrow
+// product's tile is only ~9 MFMAs.  Counts stay exact: 2^23 + 64 per MFMA of the wave < 2^24.
+#ifndef HM_MF_CONT
+#define HM_MF_CONT 1
+#endif
+struct MfCont {
+    v16f acc;
+    uint32_t prev; // bit 16 + j = bit 0 of accumulator j after the last sweep
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 8388608.0f;
+        prev = 0u;
+    }
+};
+
+template <int G>
+__device__ __forceinline__ void mf_tile_cont(const v8i (&Af)[G], const uint32_t *VI, int vlo, int T0,
+                                             int Ts, int c0, int D, uint32_t *OUT, MfCont &cs) {
+    const int lane = lane_opaque(), col = lane & 31, h = lane >> 5;
+    const uint4 *bt = (const uint4 *)VI + (32 * T0 + col - D + h + 2 * c0 - vlo);
+    constexpr int P = G < kMfPf ? G : kMfPf;
+    uint4 bq[G];
+#pragma unroll
+    for (int c = 0; c < P; ++c) bq[c] = bt[2 * c];
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+        if (c + P < G) bq[c + P] = bt[2 * (c + P)];
+        cs.acc = mfma_fp4(Af[c], b_fragment(bq[c]), cs.acc);
+        asm volatile("" : "+v"(cs.acc)::"memory");
+    }
+    const uint32_t tnow = acc_parities_hi16(cs.acc);
+    const uint32_t word = join_halves((tnow ^ cs.prev) >> (16 - 16 * h));
+    cs.prev = tnow;
+    if (h == 0) atomicXor(&OUT[32 * (T0 - Ts) + col], word); // this wave's slice only
+}
+
 // The A fragments of chunks c0 .. c0 + G - 1 from the U image RS (R words)
 template <int G>
 __device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int c0, v8i (&Af)[G]) {
@@ -104,9 +142,9 @@ __device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int 
 
 // Every tile of the span Ts .. Te - 1 that the group of G chunks from c0 reaches: two tiles at a
 // time (two accumulator chains), or (PAIRS false: 16 + 12 fewer VGPRs) one at a time
-template <int G, bool PAIRS = true>
+template <int G, bool PAIRS = true, bool CONT = false>
 __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI, int vlo, int D,
-                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
+                                         int nv, int Ts, int Te, int c0, uint32_t *OUT, MfCont &cs) {
     // tiles whose windows (words 32T - D + 2c0 .. 32T + 31 - D + 2(c0 + G) - 1) meet [0, nv)
     const int tlo = max(Ts, floor_div32(D - 2 * c0 - 2 * G + 1));
     const int thi = min(Te - 1, floor_div32(nv - 1 + D - 2 * c0));
@@ -114,18 +152,20 @@ __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI,
     if constexpr (PAIRS) {
         for (; T + 1 <= thi; T += 2) mf_tiles<G, 2>(Af, VI, vlo, T, Ts, c0, D, OUT);
         if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
+    } else if constexpr (CONT) {
+        for (; T <= thi; ++T) mf_tile_cont<G>(Af, VI, vlo, T, Ts, c0, D, OUT, cs);
     } else {
         for (; T <= thi; ++T) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
     }
 }
 
 // One group of G chunks from c0 over the tiles tlo .. thi of the span
-template <int G, bool PAIRS = true>
+template <int G, bool PAIRS, bool CONT>
 __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
-                                         int nv, int Ts, int Te, int c0, uint32_t *OUT) {
+                                         int nv, int Ts, int Te, int c0, uint32_t *OUT, MfCont &cs) {
     v8i Af[G];
     mf_afrags<G>(RS, R, D, c0, Af);
-    mf_sweep<G, PAIRS>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
+    mf_sweep<G, PAIRS, CONT>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
 }
 
 // RS quad R-1-q = the nibbles of bitreverse(U[q]) for q < ub, zero up to R, then zero to rs_words
@@ -173,12 +213,12 @@ __device__ __forceinline__ uint32_t mf_win_word(const uint32_t *Ub, int ub, int 
 }
 // wword: this lane's window word (mf_win_word, loaded ahead); the next group's is loaded here,
 // before the sweep, into *next (G2 chunks from c0 + G; G2 = 0: none)
-template <int G>
+template <int G, bool CONT>
 __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub, int ub, int G2,
                                              uint32_t *next, uint32_t *RSW, const uint32_t *tab,
                                              const uint32_t *VI, int vlo, int R, int D, int nv,
                                              int Ts, int Te, int c0, uint32_t *OUT,
-                                             const uint32_t *Ub2, int ub2) {
+                                             const uint32_t *Ub2, int ub2, MfCont &cs) {
     const int lane = lane_id();
     const int Qlo = 2 * c0 + 1;
     wsync(); // the previous group's fragment reads are done
@@ -193,7 +233,7 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
     v8i Af[G];
     mf_afrags<G>(RSW - 4 * Qlo, R, D, c0, Af);
     if (G2) *next = mf_win_word(Ub, ub, R, c0 + G, G2, Ub2, ub2);
-    mf_sweep<G, false>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT);
+    mf_sweep<G, false, CONT>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
 }
 
 #ifndef HM_MF_WPE
@@ -268,6 +308,10 @@ mul_mfma_kernel(MulMfmaArgs P) {
     uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
     for (int w = lane; w < wend - base; w += kWave) OUT[w] = 0u; // the span's live words
     const int T0 = base >> 5;
+    // (the one-tile-at-a-time instances: accumulators counting across the wave's sweeps)
+    constexpr bool CONT = LEAN && !LEAF && !WIN && HM_MF_CONT; // (the narrow instance: spills elsewhere)
+    MfCont cs;
+    if constexpr (CONT) cs.init();
     for (int b0 = 0; b0 < nu; b0 += kMfUB) {
         // U_b = words [b0, b0 + ub) of U: its product with V lands kb = b0/32 tiles up
         const int ub = min(kMfUB, nu - b0), kb = b0 >> 5;
@@ -293,17 +337,17 @@ mul_mfma_kernel(MulMfmaArgs P) {
         uint32_t ww = WIN ? mf_win_word(U + b0, ub, R, 0, gsize(0), U2 + b0, nu2 - b0) : 0u;
         for (; nc - c0 > kMfG + 1; c0 += kMfG) {
             if constexpr (WIN)
-                mf_group_win<kMfG>(ww, U + b0, ub, gsize(c0 + kMfG), &ww, RS, tab, VI, vlo, R, D, nv,
-                                   tlo, Te, c0, OUTs, U2 + b0, nu2 - b0);
-            else mf_group<kMfG, !LEAN>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);
+                mf_group_win<kMfG, CONT>(ww, U + b0, ub, gsize(c0 + kMfG), &ww, RS, tab, VI, vlo, R, D,
+                                         nv, tlo, Te, c0, OUTs, U2 + b0, nu2 - b0, cs);
+            else mf_group<kMfG, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);
         }
         switch (nc - c0) {
 #define HM_MF_TAIL(G) \
     case G:                                                                                      \
         if constexpr (WIN)                                                                       \
-            mf_group_win<G>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0, OUTs,  \
-                            U2 + b0, nu2 - b0);                                                  \
-        else mf_group<G, !LEAN>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs);                     \
+            mf_group_win<G, CONT>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0,  \
+                                  OUTs, U2 + b0, nu2 - b0, cs);                                  \
+        else mf_group<G, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);           \
         break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
             HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)
@@ -338,6 +382,7 @@ __device__ __forceinline__ void ppg_products(const MulPPGArgs &P, uint64_t e, co
     const int vlo = -D; // D <= kMfPPGWords < kVPad
     v8i Af[G];
     mf_afrags<G>(RS, R, D, 0, Af);
+    MfCont cs0; // (unused: the paired sweeps reset their accumulators per tile)
     for (uint32_t i0 = 0; i0 < grp.count; i0 += kPPGBatch) {
         const int nb = (int)min((uint32_t)kPPGBatch, grp.count - i0);
         uint32_t dv = 0u, voff = 0u, ooff = 0u, ow = 0u, oslot = 0u;
@@ -383,7 +428,7 @@ __device__ __forceinline__ void ppg_products(const MulPPGArgs &P, uint64_t e, co
             }
             for (int w = lane; w < nout; w += kWave) OUT[w] = 0u;
             wsync();
-            mf_sweep<G>(Af, VI, vlo, D, nv, 0, Te, 0, OUT);
+            mf_sweep<G>(Af, VI, vlo, D, nv, 0, Te, 0, OUT, cs0);
             wsync();
             for (int w = lane; w < nout; w += kWave) O[w] = OUT[w];
         }
