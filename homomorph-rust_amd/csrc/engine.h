@@ -199,6 +199,15 @@ constexpr int kMfSpan = 16;
 #define HM_MF_NARROW_SPAN 10
 #endif
 constexpr uint32_t kMfNarrowWords = HM_MF_NARROW_WORDS;
+// ... and within it the tiny class, U of at most kMfTinyWords words (the 17-word partial products
+// of fresh d + d' = 512 ciphertexts and carries by them, in slots of 20 words): at most
+// kMfTinyWords / 2 + 1 chunks, so its instance (mul_mfma_kernel<false, true, false, 11>) holds
+// 11 A fragments, not 17, and fits more waves per SIMD (HM_MFT_WPE)
+#ifndef HM_MF_TINY_WORDS
+#define HM_MF_TINY_WORDS 20
+#endif
+constexpr uint32_t kMfTinyWords = HM_MF_TINY_WORDS;
+constexpr int kMfTinyChunks = (int)kMfTinyWords / 2 + 1;
 constexpr uint32_t kMfNarrowSpan = HM_MF_NARROW_SPAN;
 #ifndef HM_MF_WIDE_SPAN
 #define HM_MF_WIDE_SPAN 16

@@ -99,7 +99,7 @@ struct MulPlan {
         uint32_t maxwords;         // widest prefix / result
         uint32_t prod;             // MulProdTask offset (in tasks)
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
-        MfLaunch mfl[2];                  // MFMA schoolbook products: narrow, wide
+        MfLaunch mfl[3];                  // MFMA schoolbook products: tiny, narrow, wide
         std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
@@ -415,13 +415,13 @@ bool build_plan(MulPlan &P) {
         // tiles of this column's schoolbook products: MFMA spans where the uniform operand has
         // at least kMfMinWords words (mfma plans), the rest grouped by per-lane VALU tile width
         std::vector<MulTile> byw[kNW];
-        std::vector<uint32_t> mfk[2]; // MFMA schoolbook products by class
-        uint32_t omax[2] = {0, 0};
+        std::vector<uint32_t> mfk[3]; // MFMA schoolbook products by class
+        uint32_t omax[3] = {0, 0, 0};
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
             if (is_ka[k - col.prod]) continue;
             const uint32_t uw = P.slots[P.prod[k].u].words;
             if (P.mfma && uw >= kMfMinWords) {
-                const int cl = uw <= kMfNarrowWords ? 0 : 1;
+                const int cl = uw <= kMfTinyWords ? 0 : uw <= kMfNarrowWords ? 1 : 2;
                 mfk[cl].push_back(k);
                 col.mfl[cl].vmax = std::max(col.mfl[cl].vmax, P.slots[P.prod[k].v].words);
                 col.mfl[cl].umax = std::max(col.mfl[cl].umax, uw);
@@ -439,10 +439,10 @@ bool build_plan(MulPlan &P) {
             const uint32_t span = 64 * kMulTileW[wc];
             for (uint32_t base = 0; base < nout; base += span) byw[wc].push_back({k - col.prod, base});
         }
-        for (int cl = 0; cl < 2; ++cl) {
+        for (int cl = 0; cl < 3; ++cl) {
             MfLaunch &m = col.mfl[cl];
-            m.lean = cl == 1 && kMfWideLean;
-            m.span = std::min<uint32_t>(cl ? kMfWideSpan : kMfNarrowSpan,
+            m.lean = cl == 2 && kMfWideLean;
+            m.span = std::min<uint32_t>(cl == 2 ? kMfWideSpan : kMfNarrowSpan,
                                         std::max<uint32_t>(1, (omax[cl] + 31) / 32));
             m.spans = (uint32_t)P.mspans.size();
             for (uint32_t k : mfk[cl])

@@ -254,9 +254,15 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
 //    256-word leaf's LDS slice is ~9 KB instead of ~12.5 KB and 16 waves fit a CU.
 //  - wide schoolbook products (LEAF false, WIN true: U above kMfNarrowWords) the same way as the
 //    leaves: per-group U windows, spans of kMfWideLeanSpan tiles.
-template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN>
+#ifndef HM_MFT_WPE
+#define HM_MFT_WPE 5
+#endif
+// GMAX: the most chunks any task of the launch has (the tiny class: kMfTinyChunks; otherwise any
+// count, in groups of kMfG and one tail group of at most kMfG + 1)
+template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN, int GMAX = kMfG + 1>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN, LEAN ? HM_MFN_WPE : HM_MF_WPE)))
+__attribute__((amdgpu_waves_per_eu(GMAX <= kMfG ? HM_MFT_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN,
+                                   GMAX <= kMfG ? HM_MFT_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE)))
 mul_mfma_kernel(MulMfmaArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
@@ -309,7 +315,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
     for (int w = lane; w < wend - base; w += kWave) OUT[w] = 0u; // the span's live words
     const int T0 = base >> 5;
     // (the one-tile-at-a-time instances: accumulators counting across the wave's sweeps)
-    constexpr bool CONT = LEAN && !LEAF && !WIN && HM_MF_CONT; // (the narrow instance: spills elsewhere)
+    constexpr bool CONT = LEAN && !LEAF && !WIN && GMAX > kMfG && HM_MF_CONT; // (narrow: spills elsewhere)
     MfCont cs;
     if constexpr (CONT) cs.init();
     for (int b0 = 0; b0 < nu; b0 += kMfUB) {
@@ -335,7 +341,13 @@ mul_mfma_kernel(MulMfmaArgs P) {
         // (lean leaves) each group's U window words are loaded one group ahead
         auto gsize = [&](int c) { return nc - c > kMfG + 1 ? kMfG : nc - c; };
         uint32_t ww = WIN ? mf_win_word(U + b0, ub, R, 0, gsize(0), U2 + b0, nu2 - b0) : 0u;
-        for (; nc - c0 > kMfG + 1; c0 += kMfG) {
+        if constexpr (GMAX <= kMfG) {
+            if (nc > GMAX) { // (the plan's class bound)
+                if (lane == 0) flag(P.B.status, HM_ERR_BAD_INPUT);
+                c0 = nc;
+            }
+        }
+        for (; GMAX > kMfG && nc - c0 > kMfG + 1; c0 += kMfG) {
             if constexpr (WIN)
                 mf_group_win<kMfG, CONT>(ww, U + b0, ub, gsize(c0 + kMfG), &ww, RS, tab, VI, vlo, R, D,
                                          nv, tlo, Te, c0, OUTs, U2 + b0, nu2 - b0, cs);
@@ -344,7 +356,8 @@ mul_mfma_kernel(MulMfmaArgs P) {
         switch (nc - c0) {
 #define HM_MF_TAIL(G) \
     case G:                                                                                      \
-        if constexpr (WIN)                                                                       \
+        if constexpr (G > GMAX) {                                                                \
+        } else if constexpr (WIN)                                                                \
             mf_group_win<G, CONT>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0,  \
                                   OUTs, U2 + b0, nu2 - b0, cs);                                  \
         else mf_group<G, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);           \
@@ -494,6 +507,9 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
     if (leaf && a.lean)
         hipLaunchKernelGGL((mul_mfma_kernel<true, true>), grid, block, lds, (hipStream_t)stream, a);
     else if (leaf) hipLaunchKernelGGL(mul_mfma_kernel<true>, grid, block, lds, (hipStream_t)stream, a);
+    else if (a.umax <= kMfTinyWords)
+        hipLaunchKernelGGL((mul_mfma_kernel<false, true, false, kMfTinyChunks>), grid, block, lds,
+                           (hipStream_t)stream, a);
     else if (a.umax <= kMfNarrowWords)
         hipLaunchKernelGGL((mul_mfma_kernel<false, true>), grid, block, lds, (hipStream_t)stream, a);
     else if (a.lean)
