@@ -96,7 +96,7 @@ __device__ __forceinline__ void mf_tiles(const v8i (&Af)[G], const uint32_t *VI,
 // (as the adder's chain does across tiles), so no 16 accumulator moves to 2^23 per tile -- a narrow
 // product's tile is only ~9 MFMAs.  Counts stay exact: 2^23 + 64 per MFMA of the wave < 2^24.
 #ifndef HM_MF_CONT
-#define HM_MF_CONT 1
+#define HM_MF_CONT 0 // (narrow instance: measured -1 % on the u8 multiply, its spills)
 #endif
 struct MfCont {
     v16f acc;
@@ -384,7 +384,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
 constexpr int kPPGBatch = (int)kMfPPGBatch;
 static_assert(kMfPPGWords <= 64, "one word per lane");
 
-template <int G>
+template <int G, bool PAIRS>
 __device__ __forceinline__ void ppg_products(const MulPPGArgs &P, uint64_t e, const MulPPGroup &grp,
                                              const uint32_t *RS, int nu, uint32_t du,
                                              const uint32_t *tab, uint32_t *VW, uint32_t *VI,
@@ -441,14 +441,25 @@ __device__ __forceinline__ void ppg_products(const MulPPGArgs &P, uint64_t e, co
             }
             for (int w = lane; w < nout; w += kWave) OUT[w] = 0u;
             wsync();
-            mf_sweep<G>(Af, VI, vlo, D, nv, 0, Te, 0, OUT, cs0);
+            mf_sweep<G, PAIRS>(Af, VI, vlo, D, nv, 0, Te, 0, OUT, cs0);
             wsync();
             for (int w = lane; w < nout; w += kWave) O[w] = OUT[w];
         }
     }
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HM_MF_WPE_MIN, HM_MF_WPE)))
+#ifndef HM_PPG_NO_TINY
+#define HM_PPG_NO_TINY 0 // (A/B knob) the partial products on the general instance only
+#endif
+#ifndef HM_PPGT_WPE
+#define HM_PPGT_WPE 4
+#endif
+// GMAX: the most chunks of any a_j (kMfTinyChunks: a_j within kMfTinyWords words, the fresh
+// operands of d + d' <= 512 -- an instance with 11 A fragments and one tile at a time, the products'
+// outputs being one or two tiles, at HM_MFT_WPE waves per SIMD instead of 3)
+template <int GMAX>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(GMAX <= kMfG ? HM_PPGT_WPE : HM_MF_WPE_MIN, GMAX <= kMfG ? HM_PPGT_WPE : HM_MF_WPE)))
 mul_ppg_kernel(MulPPGArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
@@ -463,14 +474,15 @@ mul_ppg_kernel(MulPPGArgs P) {
     uint32_t *arena = P.B.arena + e * P.B.astride;
     const uint32_t du = rfl(P.B.deg1[(uint64_t)grp.u * P.B.nv + e]);
     const int nu = bitwords((int)du);
-    if (nu == 0 || nu > (int)kMfPPGWords) { // null a_j: every product of the group is null
+    constexpr int kUMax = GMAX <= kMfG ? (int)kMfTinyWords : (int)kMfPPGWords; // (the plan's bound)
+    if (nu == 0 || nu > kUMax) { // null a_j: every product of the group is null
         for (uint32_t it = 0; it < grp.count; ++it) {
             const MulPPItem item = P.items[grp.first + it];
             uint32_t *O = arena + P.B.slots[item.out].off;
             for (int w = lane; w < (int)P.B.slots[item.out].words; w += kWave) O[w] = 0u;
             if (lane == 0) P.B.deg1[(uint64_t)item.out * P.B.nv + e] = 0u;
         }
-        if (nu > (int)kMfPPGWords && lane == 0) flag(P.B.status, HM_ERR_BAD_INPUT); // (plan bound)
+        if (nu > kUMax && lane == 0) flag(P.B.status, HM_ERR_BAD_INPUT); // (plan bound)
         return;
     }
     uint32_t *RS = lds + 256 + (size_t)wave * P.wave_words;
@@ -482,7 +494,9 @@ mul_ppg_kernel(MulPPGArgs P) {
     wsync();
     switch (nu / 2 + 1) {
 #define HM_PPG(G) \
-    case G: ppg_products<G>(P, e, grp, RS, nu, du, tab, VW, VI, OUT); break;
+    case G:                                                                                      \
+        if constexpr (G <= GMAX) ppg_products<G, (GMAX > kMfG)>(P, e, grp, RS, nu, du, tab, VW, VI, OUT); \
+        break;
         HM_PPG(1) HM_PPG(2) HM_PPG(3) HM_PPG(4) HM_PPG(5) HM_PPG(6) HM_PPG(7) HM_PPG(8) HM_PPG(9)
         HM_PPG(10) HM_PPG(11) HM_PPG(12) HM_PPG(13) HM_PPG(14) HM_PPG(15) HM_PPG(16) HM_PPG(17)
 #undef HM_PPG
@@ -494,7 +508,10 @@ int launch_mul_ppg(const MulPPGArgs &a, void *stream) {
     const uint64_t waves = a.B.nv * a.ngroups;
     if (!waves) return 0;
     const size_t lds = (256 + (size_t)a.wave_words * 4) * 4;
-    hipLaunchKernelGGL(mul_ppg_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+    if (a.umax <= kMfTinyWords && !HM_PPG_NO_TINY)
+        hipLaunchKernelGGL(mul_ppg_kernel<kMfTinyChunks>, dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+                           (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(mul_ppg_kernel<kMfG + 1>, dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
                        (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
