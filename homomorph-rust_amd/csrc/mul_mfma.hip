@@ -142,7 +142,7 @@ __device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int 
 
 // Every tile of the span Ts .. Te - 1 that the group of G chunks from c0 reaches: two tiles at a
 // time (two accumulator chains), or (PAIRS false: 16 + 12 fewer VGPRs) one at a time
-template <int G, bool PAIRS = true, bool CONT = false>
+template <int G, bool PAIRS = true, bool CONT = false, bool TRIM = false>
 __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI, int vlo, int D,
                                          int nv, int Ts, int Te, int c0, uint32_t *OUT, MfCont &cs) {
     // tiles whose windows (words 32T - D + 2c0 .. 32T + 31 - D + 2(c0 + G) - 1) meet [0, nv)
@@ -154,18 +154,30 @@ __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI,
         if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
     } else if constexpr (CONT) {
         for (; T <= thi; ++T) mf_tile_cont<G>(Af, VI, vlo, T, Ts, c0, D, OUT, cs);
+    } else if constexpr (TRIM) {
+        // (tiny products) a tile whose windows leave V after the first ch < G chunks runs only
+        // those: the top tile of a 17 x 17-word product (33 output words) needs 1 chunk, not 9
+        for (; T <= thi; ++T) {
+            const int ch = ((nv - 1 + D - 32 * T - 2 * c0) >> 1) + 1; // chunks c0 .. c0 + ch - 1
+            switch (ch < G ? ch : 0) {
+            case 1: mf_tiles<1, 1>((const v8i(&)[1])Af, VI, vlo, T, Ts, c0, D, OUT); break;
+            case 2: mf_tiles<2, 1>((const v8i(&)[2])Af, VI, vlo, T, Ts, c0, D, OUT); break;
+            case 3: mf_tiles<3, 1>((const v8i(&)[3])Af, VI, vlo, T, Ts, c0, D, OUT); break;
+            default: mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT); break;
+            }
+        }
     } else {
         for (; T <= thi; ++T) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
     }
 }
 
 // One group of G chunks from c0 over the tiles tlo .. thi of the span
-template <int G, bool PAIRS, bool CONT>
+template <int G, bool PAIRS, bool CONT, bool TRIM = false>
 __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
                                          int nv, int Ts, int Te, int c0, uint32_t *OUT, MfCont &cs) {
     v8i Af[G];
     mf_afrags<G>(RS, R, D, c0, Af);
-    mf_sweep<G, PAIRS, CONT>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
+    mf_sweep<G, PAIRS, CONT, TRIM>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
 }
 
 // RS quad R-1-q = the nibbles of bitreverse(U[q]) for q < ub, zero up to R, then zero to rs_words
@@ -254,6 +266,9 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
 //    256-word leaf's LDS slice is ~9 KB instead of ~12.5 KB and 16 waves fit a CU.
 //  - wide schoolbook products (LEAF false, WIN true: U above kMfNarrowWords) the same way as the
 //    leaves: per-group U windows, spans of kMfWideLeanSpan tiles.
+#ifndef HM_MF_TRIM
+#define HM_MF_TRIM 1 // tiny instance: tiles that need fewer chunks than the group run only those
+#endif
 #ifndef HM_MFT_WPE
 #define HM_MFT_WPE 5
 #endif
@@ -360,7 +375,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
         } else if constexpr (WIN)                                                                \
             mf_group_win<G, CONT>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0,  \
                                   OUTs, U2 + b0, nu2 - b0, cs);                                  \
-        else mf_group<G, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);           \
+        else mf_group<G, !LEAN, CONT, (GMAX <= kMfG && HM_MF_TRIM)>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs); \
         break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
             HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)

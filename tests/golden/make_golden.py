@@ -26,7 +26,8 @@ for p in (ROOT, os.path.join(ROOT, "homomorph-rust_amd"), os.path.join(ROOT, "te
     if p not in sys.path:
         sys.path.insert(0, p)
 
-from helpers import as_bytes, bit_ints, fresh_bound, low_bits, masks, plain, digest  # noqa: E402
+from helpers import (as_bytes, bit_ints, fresh_bound, low_bits, masks, pad_bits_host, plain,  # noqa: E402
+                     digest)
 from oracle import gf2_model as model  # noqa: E402
 from oracle import oracle_py as oracle  # noqa: E402
 
@@ -112,9 +113,13 @@ def make(name):
         oracle.set_threads(n)
         lo, do = oracle.mul_batch(l1, d1, b1, l2, d2, b2, k, n, ob)
         oracle.set_threads(1)
-        dec = oracle.decrypt_batch(sk, lo, do, ob, k, n).reshape(n, k // 8)
+        # (K = 20 takes the oracle hours: keep the product before anything else can fail)
+        np.savez(os.path.join(HERE, f".{name}_product.npz"), lo=lo, do=do, ob=ob)
+        kb = (k + 7) // 8  # decrypted as whole bytes: bits k .. 8 kb - 1 are null polynomials
+        pl, pd, pb = pad_bits_host(lo, do, ob, n, 8 * kb)
+        dec = oracle.decrypt_batch(sk, pl, pd, pb, 8 * kb, n).reshape(n, kb)
         val = np.zeros(n, dtype=np.uint64)
-        for byte in range(k // 8):
+        for byte in range(kb):
             val |= dec[:, byte].astype(np.uint64) << np.uint64(8 * byte)
         out.update(k=np.array(k), out_bound=ob, out_degree=do,
                    out_sha256=np.array(digest(lo, ob, n)), out_plain=val,

@@ -60,6 +60,18 @@ def assert_batches_equal(l1, d1, l2, d2, bound, n, what=""):
         raise AssertionError(f"{what}: limb mismatch at {bad.tolist()} (value {bad // stride})")
 
 
+def pad_bits_host(limbs, deg, bound, n, nbits):
+    """A host batch widened to nbits ciphertext bits per value, the new bits null polynomials
+    (bound 0, one zero limb): a k-bit product decrypted as whole bytes (k % 8 != 0)."""
+    _, _, stride = offsets(bound)
+    extra = int(nbits) - len(bound)
+    l = np.concatenate([np.asarray(limbs, dtype=np.uint64).reshape(n, stride),
+                        np.zeros((n, extra), dtype=np.uint64)], axis=1).reshape(-1)
+    d = np.concatenate([np.asarray(deg, dtype=np.uint32).reshape(n, len(bound)),
+                        np.zeros((n, extra), dtype=np.uint32)], axis=1).reshape(-1)
+    return l, d, np.concatenate([np.asarray(bound, dtype=np.uint32), np.zeros(extra, dtype=np.uint32)])
+
+
 def digest(limbs, bound, n):
     """Per-value SHA-256 (hex) of a batch's limbs (the batch layout, capacity limbs per bit)."""
     import hashlib

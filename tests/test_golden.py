@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import as_bytes, assert_batches_equal, digest, low_bits
+from helpers import as_bytes, assert_batches_equal, digest, low_bits, pad_bits_host
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FIXTURES = sorted(os.path.splitext(os.path.basename(p))[0]
@@ -60,7 +60,9 @@ def test_oracle_reproduces_golden(oracle, name):
             oracle.set_threads(1)
         assert np.array_equal(do, g["out_degree"])
         assert digest(lo, ob, n) == [str(x) for x in g["out_sha256"]]
-        _check_mullow_plain(g, oracle.decrypt_batch(sk, lo, do, ob, k, n), k, n)
+        kb = (k + 7) // 8
+        _check_mullow_plain(g, oracle.decrypt_batch(sk, *pad_bits_host(lo, do, ob, n, 8 * kb), 8 * kb, n),
+                            k, n)
         return
     if op == "add":
         lo, do = oracle.add_batch(la, da, bound, lb, db, bound, nbits, n, ob)
@@ -80,9 +82,10 @@ def _check_mullow_plain(g, dec, k, n):
     """The decryption matches the fixture's (oracle) decryption; at d = 128 the scheme's noise
     outgrows the key in the deep columns of the multiplier, so only the low result bits decrypt
     to a*b (the ciphertexts are bit-exact either way)."""
-    dec = np.asarray(dec).reshape(n, k // 8)
+    kb = (k + 7) // 8  # (k % 8 != 0: decrypted through null pad bits)
+    dec = np.asarray(dec).reshape(n, kb)
     val = np.zeros(n, dtype=np.uint64)
-    for byte in range(k // 8):
+    for byte in range(kb):
         val |= dec[:, byte].astype(np.uint64) << np.uint64(8 * byte)
     assert np.array_equal(val, g["out_plain"])
     assert np.array_equal(val & 0xFF, g["expected_plain"] & 0xFF)
@@ -113,7 +116,7 @@ def test_gpu_reproduces_golden(name):
         ol, od = out.to_host()
         assert np.array_equal(od, g["out_degree"]), name + " gpu degrees"
         assert digest(ol, out.bound, n) == [str(x) for x in g["out_sha256"]], name + " gpu limbs"
-        _check_mullow_plain(g, ctx.decrypt_bytes(out).cpu().numpy(), k, n)
+        _check_mullow_plain(g, ctx.decrypt_bytes(H.pad_bits(out, 8 * ((k + 7) // 8))).cpu().numpy(), k, n)
         return
     if op == "encdec":
         out = a
