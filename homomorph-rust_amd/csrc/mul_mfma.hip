@@ -273,11 +273,17 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
 #define HM_MFT_WPE 5
 #endif
 // GMAX: the most chunks any task of the launch has (the tiny class: kMfTinyChunks; otherwise any
-// count, in groups of kMfG and one tail group of at most kMfG + 1)
-template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN, int GMAX = kMfG + 1>
+// count, in groups of GS and one tail group of at most GS + 1)
+#ifndef HM_MFNS_WPE
+#define HM_MFNS_WPE 5 // waves per SIMD of the narrow instance with groups smaller than kMfG
+#endif
+#ifndef HM_MFN_GS
+#define HM_MFN_GS 16 // chunks per group of the narrow instance (A fragments held: GS + 1)
+#endif
+template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN, int GMAX = kMfG + 1, int GS = kMfG>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(GMAX <= kMfG ? HM_MFT_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN,
-                                   GMAX <= kMfG ? HM_MFT_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE)))
+__attribute__((amdgpu_waves_per_eu(GMAX <= kMfG ? HM_MFT_WPE : GS < kMfG ? HM_MFNS_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN,
+                                   GMAX <= kMfG ? HM_MFT_WPE : GS < kMfG ? HM_MFNS_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE)))
 mul_mfma_kernel(MulMfmaArgs P) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
@@ -330,7 +336,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
     for (int w = lane; w < wend - base; w += kWave) OUT[w] = 0u; // the span's live words
     const int T0 = base >> 5;
     // (the one-tile-at-a-time instances: accumulators counting across the wave's sweeps)
-    constexpr bool CONT = LEAN && !LEAF && !WIN && GMAX > kMfG && HM_MF_CONT; // (narrow: spills elsewhere)
+    constexpr bool CONT = LEAN && !LEAF && !WIN && GMAX > GS && HM_MF_CONT; // (narrow: spills elsewhere)
     MfCont cs;
     if constexpr (CONT) cs.init();
     for (int b0 = 0; b0 < nu; b0 += kMfUB) {
@@ -354,28 +360,29 @@ mul_mfma_kernel(MulMfmaArgs P) {
         // one per 4-chunk group, and a 256-word leaf's 129 chunks end in a 17-chunk group
         int c0 = 0;
         // (lean leaves) each group's U window words are loaded one group ahead
-        auto gsize = [&](int c) { return nc - c > kMfG + 1 ? kMfG : nc - c; };
+        auto gsize = [&](int c) { return nc - c > GS + 1 ? GS : nc - c; };
         uint32_t ww = WIN ? mf_win_word(U + b0, ub, R, 0, gsize(0), U2 + b0, nu2 - b0) : 0u;
-        if constexpr (GMAX <= kMfG) {
+        static_assert(!WIN || GS == kMfG, "the windowed instances' LDS is sized for kMfG + 1");
+        if constexpr (GMAX <= GS) {
             if (nc > GMAX) { // (the plan's class bound)
                 if (lane == 0) flag(P.B.status, HM_ERR_BAD_INPUT);
                 c0 = nc;
             }
         }
-        for (; GMAX > kMfG && nc - c0 > kMfG + 1; c0 += kMfG) {
+        for (; GMAX > GS && nc - c0 > GS + 1; c0 += GS) {
             if constexpr (WIN)
-                mf_group_win<kMfG, CONT>(ww, U + b0, ub, gsize(c0 + kMfG), &ww, RS, tab, VI, vlo, R, D,
-                                         nv, tlo, Te, c0, OUTs, U2 + b0, nu2 - b0, cs);
-            else mf_group<kMfG, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);
+                mf_group_win<GS, CONT>(ww, U + b0, ub, gsize(c0 + GS), &ww, RS, tab, VI, vlo, R, D,
+                                       nv, tlo, Te, c0, OUTs, U2 + b0, nu2 - b0, cs);
+            else mf_group<GS, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);
         }
         switch (nc - c0) {
 #define HM_MF_TAIL(G) \
     case G:                                                                                      \
-        if constexpr (G > GMAX) {                                                                \
+        if constexpr (G > GMAX || G > GS + 1) {                                                  \
         } else if constexpr (WIN)                                                                \
             mf_group_win<G, CONT>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0,  \
                                   OUTs, U2 + b0, nu2 - b0, cs);                                  \
-        else mf_group<G, !LEAN, CONT, (GMAX <= kMfG && HM_MF_TRIM)>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs); \
+        else mf_group<G, !LEAN, CONT, (GMAX <= GS && HM_MF_TRIM)>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs); \
         break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
             HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)
@@ -543,7 +550,8 @@ int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
         hipLaunchKernelGGL((mul_mfma_kernel<false, true, false, kMfTinyChunks>), grid, block, lds,
                            (hipStream_t)stream, a);
     else if (a.umax <= kMfNarrowWords)
-        hipLaunchKernelGGL((mul_mfma_kernel<false, true>), grid, block, lds, (hipStream_t)stream, a);
+        hipLaunchKernelGGL((mul_mfma_kernel<false, true, false, kMfG + 1, HM_MFN_GS>), grid, block, lds,
+                           (hipStream_t)stream, a);
     else if (a.lean)
         hipLaunchKernelGGL((mul_mfma_kernel<false, true, true>), grid, block, lds, (hipStream_t)stream, a);
     else hipLaunchKernelGGL(mul_mfma_kernel<false>, grid, block, lds, (hipStream_t)stream, a);
