@@ -26,6 +26,20 @@
 namespace hm {
 
 constexpr int kMfG = 16;      // chunks per full A group (64 VGPRs of A fragments)
+
+// Phase timers (diagnostic builds with -DHM_MF_PROFILE only; the library never has them): per
+// launch class (the instance's template key), s_memtime deltas summed over waves for the record
+// loads, the operand images, the chunk groups (A fragments + tiles) and the copy-out, plus the
+// wave count; read back with hm_debug_mf_prof (scripts/mf_phases.py).
+#ifdef HM_MF_PROFILE
+__device__ unsigned long long g_mf_prof[8][8];
+#define HM_MF_PT(v)                                                                               \
+    asm volatile("" ::: "memory");                                                                \
+    const unsigned long long v = __builtin_amdgcn_s_memtime();                                    \
+    asm volatile("" ::: "memory")
+#else
+#define HM_MF_PT(v)
+#endif
 #ifndef HM_MF_PF
 #define HM_MF_PF 3
 #endif
@@ -294,6 +308,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
     const uint64_t e = g / P.nitems;
     if (e >= P.B.nv) return; // whole wave exits together
     const uint32_t item = (uint32_t)(g % P.nitems);
+    HM_MF_PT(tp0);
     uint32_t *arena = P.B.arena + e * P.B.astride;
     const uint32_t *U, *V, *U2 = nullptr, *V2 = nullptr;
     uint32_t *O;
@@ -335,6 +350,11 @@ mul_mfma_kernel(MulMfmaArgs P) {
     uint32_t *OUT = VI + mf_vi_words(P.vmax, P.span, P.umax);
     for (int w = lane; w < wend - base; w += kWave) OUT[w] = 0u; // the span's live words
     const int T0 = base >> 5;
+#ifdef HM_MF_PROFILE
+    (void)rfl((uint32_t)(uintptr_t)U); // the record loads have landed
+    HM_MF_PT(tp1);
+    unsigned long long t_img = 0, t_grp = 0;
+#endif
     // (the one-tile-at-a-time instances: accumulators counting across the wave's sweeps)
     constexpr bool CONT = LEAN && !LEAF && !WIN && GMAX > GS && HM_MF_CONT; // (narrow: spills elsewhere)
     MfCont cs;
@@ -349,9 +369,15 @@ mul_mfma_kernel(MulMfmaArgs P) {
         const int vhi = min(32 * Te + 32 - D + 2 * nc, nv + kVPad);
         wsync(); // the previous block's reads of RS / VI are done
         // RS quad R-1-q = the nibbles of bitreverse(U_b[q]) (one load, one 16-B store per word)
+        HM_MF_PT(tpa);
         if constexpr (!WIN) mf_u_image(U + b0, ub, R, rs_words, tab, RS, U2 + b0, nu2 - b0);
         mf_v_image(V, nv, vlo, vhi, tab, VI, V2, nv2);
         wsync();
+#ifdef HM_MF_PROFILE
+        __builtin_amdgcn_s_waitcnt(0); // (the image stores)
+        HM_MF_PT(tpb);
+        t_img += tpb - tpa;
+#endif
         const int tlo = max(Ts, 0);
         uint32_t *OUTs = OUT + 32 * (tlo - Ts);
         // groups of 16 chunks while more than 17 are left, then the rest as ONE group of 1..17
@@ -390,9 +416,26 @@ mul_mfma_kernel(MulMfmaArgs P) {
 #undef HM_MF_TAIL
         default: break;
         }
+#ifdef HM_MF_PROFILE
+        HM_MF_PT(tpc);
+        t_grp += tpc - tpb;
+#endif
     }
     wsync();
     for (int w = base + lane; w < wend; w += kWave) O[w] = OUT[w - base];
+#ifdef HM_MF_PROFILE
+    __builtin_amdgcn_s_waitcnt(0);
+    HM_MF_PT(tp9);
+    if (lane == 0) {
+        // class: 0 leaves, 1 lean leaves, 2 tiny, 3 narrow, 4 wide (windowed), 5 wide
+        const int cls = LEAF ? (LEAN ? 1 : 0) : (GMAX <= kMfG ? 2 : (LEAN && !WIN) ? 3 : WIN ? 4 : 5);
+        atomicAdd(&g_mf_prof[cls][0], 1ull);
+        atomicAdd(&g_mf_prof[cls][1], tp1 - tp0);       // records, degrees, OUT zero
+        atomicAdd(&g_mf_prof[cls][2], t_img);           // operand images
+        atomicAdd(&g_mf_prof[cls][3], t_grp);           // A fragments + tiles
+        atomicAdd(&g_mf_prof[cls][4], tp9 - tp1 - t_img - t_grp); // copy-out and the rest
+    }
+#endif
 }
 
 // Partial products a_j * b_k grouped by a_j (MulPPGroup): one wave per (value, group).  a_j has
@@ -567,3 +610,14 @@ uint32_t mul_mfma_lean_leaf_wave_words(uint32_t vmax, uint32_t span, uint32_t um
 }
 
 } // namespace hm
+
+#ifdef HM_MF_PROFILE
+extern "C" int hm_debug_mf_prof(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hm::g_mf_prof), sizeof(hm::g_mf_prof)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[8][8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hm::g_mf_prof), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
