@@ -147,6 +147,16 @@ struct MulProdTask {
 struct MulTile {
     uint32_t task, base; // output words [base, base + 64 W) of task
 };
+// One span of an MFMA schoolbook product, resolved on the host (mul_host.cpp build_plan): the
+// operands' and the output's arena offsets and the operands' sizes from their STATIC bounds (slots
+// are zero above their degree up to their capacity, so the words up to the bound are the
+// polynomial), so a wave issues its operand loads right after this one record instead of after
+// the span -> task -> degree / slot chain; the degrees only give the output's degree, at the end.
+struct MulSpanRec {
+    uint32_t uoff, voff, ooff, nout; // arena offsets; output slot capacity (words)
+    uint32_t nu, nv, base, oslot;    // operand words at their bounds; first output word; out slot
+    uint32_t uslot, vslot, _p0, _p1; // operand slots (their degrees make the output's)
+};
 struct MulProdArgs {
     MulBase B;
     const MulProdTask *tasks;
@@ -231,6 +241,7 @@ struct MulMfmaArgs {
     MulBase B;
     const void *tasks;
     const MulTile *spans; // schoolbook products: {task, base}
+    const MulSpanRec *recs; // ... the same spans resolved (MulSpanRec), used by the MFMA kernels
     uint32_t nitems;      // work items per value (leaves: tasks x nspans)
     uint32_t nspans;      // leaves: spans per task
     uint32_t span;        // output tiles per span

@@ -110,6 +110,8 @@ struct MulPlan {
     std::vector<MulProdTask> prod;
     std::vector<MulTile> tiles;
     std::vector<MulTile> mspans; // MFMA spans {task, first output word} of the schoolbook products
+    std::vector<MulSpanRec> mrecs; // ... resolved (parallel to mspans; built after the regions)
+    std::vector<int64_t> slot_bound; // each slot's static degree bound (-1: always null)
     std::vector<MulProdTask> ppm; // partial products a_j * b_k run on the matrix cores
     // ... or, when every one fits (kMfPPGWords), all of them in one launch before the columns,
     // grouped by a_j (mul_ppg_kernel)
@@ -125,7 +127,7 @@ struct MulPlan {
     uint8_t *d_tab = nullptr;
     size_t tab_bytes = 0;
     size_t off_slots = 0, off_pp = 0, off_lists = 0, off_prod = 0, off_tiles = 0, off_res = 0;
-    size_t off_mspans = 0, off_ppm = 0;
+    size_t off_mspans = 0, off_ppm = 0, off_mrecs = 0;
     size_t off_ka_sums = 0, off_ka_vtasks = 0, off_ka_vtiles = 0, off_ka_combs = 0;
     uint64_t work = 0; // word-pair products (statistics)
     std::vector<double> prod_pairs; // per carry product (P.prod): its schoolbook word pairs
@@ -234,6 +236,7 @@ bool build_plan(MulPlan &P) {
     auto new_slot = [&](int r, int64_t bound) -> uint32_t {
         const uint32_t w = bound < 0 ? 0u : slot_words(bound);
         P.slots.push_back({(uint32_t)reg[r].used, w});
+        P.slot_bound.push_back(bound);
         slot_reg.push_back((uint8_t)r);
         reg[r].used += w;
         reg[r].max = std::max(reg[r].max, reg[r].used);
@@ -477,6 +480,22 @@ bool build_plan(MulPlan &P) {
         t.u = fix(t.u), t.v = fix(t.v), t.out = fix(t.out), t.u2 = fix(t.u2), t.v2 = fix(t.v2);
     for (auto &t : P.ka_combs) t.z0 = fix(t.z0), t.z1 = fix(t.z1), t.z2 = fix(t.z2), t.r = fix(t.r);
     P.astride = std::max<uint64_t>(base, 4);
+    // the MFMA spans resolved: every launch's span range of mspans, task indices relative to the
+    // column's product list (ppm for the partial products' launch, prod for the carries)
+    P.mrecs.assign(P.mspans.size(), MulSpanRec{});
+    auto bw = [&](uint32_t s) { return P.slot_bound[s] < 0 ? 0u : (uint32_t)(P.slot_bound[s] / 32 + 1); };
+    auto resolve = [&](const MfLaunch &m, const std::vector<MulProdTask> &tasks, uint32_t t0) {
+        for (uint32_t i = m.spans; i < m.spans + m.nspans; ++i) {
+            const MulProdTask &t = tasks[t0 + P.mspans[i].task];
+            P.mrecs[i] = MulSpanRec{P.slots[t.u].off, P.slots[t.v].off, P.slots[t.out].off,
+                                    P.slots[t.out].words, bw(t.u), bw(t.v), P.mspans[i].base, t.out,
+                                    t.u, t.v, 0u, 0u};
+        }
+    };
+    for (const auto &col : P.cols) {
+        resolve(col.ppl, P.ppm, col.ppm);
+        for (const MfLaunch &m : col.mfl) resolve(m, P.prod, col.prod);
+    }
     return true;
 }
 
@@ -490,6 +509,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
     P.off_mspans = o, o = align(o + P.mspans.size() * sizeof(MulTile));
+    P.off_mrecs = o, o = align(o + P.mrecs.size() * sizeof(MulSpanRec));
     P.off_ppm = o, o = align(o + P.ppm.size() * sizeof(MulProdTask));
     P.off_ppg_groups = o, o = align(o + P.ppg_groups.size() * sizeof(MulPPGroup));
     P.off_ppg_items = o, o = align(o + P.ppg_items.size() * sizeof(MulPPItem));
@@ -508,6 +528,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
     put(P.off_mspans, P.mspans.data(), P.mspans.size() * sizeof(MulTile));
+    put(P.off_mrecs, P.mrecs.data(), P.mrecs.size() * sizeof(MulSpanRec));
     put(P.off_ppm, P.ppm.data(), P.ppm.size() * sizeof(MulProdTask));
     put(P.off_ppg_groups, P.ppg_groups.data(), P.ppg_groups.size() * sizeof(MulPPGroup));
     put(P.off_ppg_items, P.ppg_items.data(), P.ppg_items.size() * sizeof(MulPPItem));
@@ -731,6 +752,7 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 MulMfmaArgs mf{};
                 mf.B = B, mf.tasks = (const MulProdTask *)(T + task_off) + task0;
                 mf.spans = (const MulTile *)(T + P->off_mspans) + m.spans;
+                mf.recs = (const MulSpanRec *)(T + P->off_mrecs) + m.spans;
                 mf.nitems = m.nspans, mf.span = m.span;
                 mf.vmax = m.vmax, mf.umax = m.umax;
                 mf.wave_words = mul_mfma_wave_words(mf.vmax, mf.span, mf.umax);

@@ -194,19 +194,34 @@ __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI,
     mf_sweep<G, PAIRS, CONT, TRIM>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
 }
 
+#ifndef HM_MF_IMG_BATCH
+#define HM_MF_IMG_BATCH 4
+#endif
+constexpr int kMfImgBatch = HM_MF_IMG_BATCH; // operand words per lane loaded together (images)
 // RS quad R-1-q = the nibbles of bitreverse(U[q]) for q < ub, zero up to R, then zero to rs_words
 // (U2: a second view XORed in below ub2, a fused Karatsuba sum; ub2 <= 0: none)
 __device__ __forceinline__ void mf_u_image(const uint32_t *U, int ub, int R, uint32_t rs_words,
                                            const uint32_t *tab, uint32_t *RS,
                                            const uint32_t *U2 = nullptr, int ub2 = 0) {
     const int lane = lane_id();
-    for (int q = lane; q < R; q += kWave) {
-        const uint32_t rev =
-            q < ub ? __builtin_bitreverse32(U[q] ^ (q < ub2 ? U2[q] : 0u)) : 0u;
-        uint4 x;
-        x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
-        x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
-        ((uint4 *)RS)[R - 1 - q] = x;
+    // the lane's words are all loaded before any is converted (kMfImgBatch in flight per lane)
+    for (int q0 = 0; q0 < R; q0 += kWave * kMfImgBatch) {
+        uint32_t u[kMfImgBatch];
+#pragma unroll
+        for (int k = 0; k < kMfImgBatch; ++k) {
+            const int q = q0 + lane + kWave * k;
+            u[k] = q < ub ? U[q] ^ (q < ub2 ? U2[q] : 0u) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kMfImgBatch; ++k) {
+            const int q = q0 + lane + kWave * k;
+            if (q >= R) break;
+            const uint32_t rev = __builtin_bitreverse32(u[k]);
+            uint4 x;
+            x.x = tab[rev & 0xFFu], x.y = tab[(rev >> 8) & 0xFFu];
+            x.z = tab[(rev >> 16) & 0xFFu], x.w = tab[rev >> 24];
+            ((uint4 *)RS)[R - 1 - q] = x;
+        }
     }
     for (int k = 4 * R + lane; k < (int)rs_words; k += kWave) RS[k] = 0u;
 }
@@ -216,13 +231,22 @@ __device__ __forceinline__ void mf_v_image(const uint32_t *V, int nv, int vlo, i
                                            const uint32_t *tab, uint32_t *VI,
                                            const uint32_t *V2 = nullptr, int nv2 = 0) {
     const int lane = lane_id();
-    for (int i = lane; i < vhi - vlo; i += kWave) {
-        const int w = vlo + i;
-        const uint32_t v = (w >= 0 && w < nv) ? V[w] ^ (w < nv2 ? V2[w] : 0u) : 0u;
-        uint4 q;
-        q.x = tab[v & 0xFFu], q.y = tab[(v >> 8) & 0xFFu];
-        q.z = tab[(v >> 16) & 0xFFu], q.w = tab[v >> 24];
-        ((uint4 *)VI)[i] = q;
+    for (int i0 = 0; i0 < vhi - vlo; i0 += kWave * kMfImgBatch) {
+        uint32_t v[kMfImgBatch];
+#pragma unroll
+        for (int k = 0; k < kMfImgBatch; ++k) {
+            const int w = vlo + i0 + lane + kWave * k;
+            v[k] = (w >= 0 && w < nv && w < vhi) ? V[w] ^ (w < nv2 ? V2[w] : 0u) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kMfImgBatch; ++k) {
+            const int i = i0 + lane + kWave * k;
+            if (i >= vhi - vlo) break;
+            uint4 q;
+            q.x = tab[v[k] & 0xFFu], q.y = tab[(v[k] >> 8) & 0xFFu];
+            q.z = tab[(v[k] >> 16) & 0xFFu], q.w = tab[v[k] >> 24];
+            ((uint4 *)VI)[i] = q;
+        }
     }
 }
 
@@ -323,16 +347,18 @@ mul_mfma_kernel(MulMfmaArgs P) {
         U2 = arena + (nu2 ? t.u2 : t.u), V2 = arena + (nv2 ? t.v2 : t.v);
         if (base >= nout) return;
     } else {
-        const MulTile tl = P.spans[item];
-        const MulProdTask t = ((const MulProdTask *)P.tasks)[tl.task];
-        base = (int)rfl(tl.base);
-        const uint32_t du = rfl(P.B.deg1[(uint64_t)t.u * P.B.nv + e]);
-        const uint32_t dv = rfl(P.B.deg1[(uint64_t)t.v * P.B.nv + e]);
-        U = arena + P.B.slots[t.u].off, V = arena + P.B.slots[t.v].off;
-        O = arena + P.B.slots[t.out].off;
-        nu = bitwords((int)du), nv = bitwords((int)dv), nout = (int)P.B.slots[t.out].words;
-        if (base == 0 && lane_id() == 0)
-            P.B.deg1[(uint64_t)t.out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+        // one resolved record (MulSpanRec): operand sizes from the static bounds, so the operand
+        // loads go out right after it; the degrees (loaded now, used at the end) only make the
+        // output's degree
+        const MulSpanRec r = P.recs[item];
+        base = (int)rfl(r.base);
+        U = arena + r.uoff, V = arena + r.voff, O = arena + r.ooff;
+        nu = (int)rfl(r.nu), nv = (int)rfl(r.nv), nout = (int)rfl(r.nout);
+        if (base == 0) {
+            const uint32_t du = P.B.deg1[(uint64_t)r.uslot * P.B.nv + e];
+            const uint32_t dv = P.B.deg1[(uint64_t)r.vslot * P.B.nv + e];
+            if (lane_id() == 0) P.B.deg1[(uint64_t)r.oslot * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+        }
     }
     if (!nu2) U2 = U; // (never read: a valid pointer all the same)
     if (!nv2) V2 = V;
