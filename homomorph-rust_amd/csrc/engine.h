@@ -148,14 +148,12 @@ struct MulTile {
     uint32_t task, base; // output words [base, base + 64 W) of task
 };
 // One span of an MFMA schoolbook product, resolved on the host (mul_host.cpp build_plan): the
-// operands' and the output's arena offsets and the operands' sizes from their STATIC bounds (slots
-// are zero above their degree up to their capacity, so the words up to the bound are the
-// polynomial), so a wave issues its operand loads right after this one record instead of after
-// the span -> task -> degree / slot chain; the degrees only give the output's degree, at the end.
+// operands' and the output's arena offsets and slots, so a wave's only dependent loads after this
+// one record are the operands' degrees (instead of span -> task -> slots -> degrees).
 struct MulSpanRec {
     uint32_t uoff, voff, ooff, nout; // arena offsets; output slot capacity (words)
-    uint32_t nu, nv, base, oslot;    // operand words at their bounds; first output word; out slot
-    uint32_t uslot, vslot, _p0, _p1; // operand slots (their degrees make the output's)
+    uint32_t uslot, vslot, oslot;    // slots (the operands' degrees; the output's, written)
+    uint32_t base;                   // first output word of the span
 };
 struct MulProdArgs {
     MulBase B;

@@ -111,7 +111,6 @@ struct MulPlan {
     std::vector<MulTile> tiles;
     std::vector<MulTile> mspans; // MFMA spans {task, first output word} of the schoolbook products
     std::vector<MulSpanRec> mrecs; // ... resolved (parallel to mspans; built after the regions)
-    std::vector<int64_t> slot_bound; // each slot's static degree bound (-1: always null)
     std::vector<MulProdTask> ppm; // partial products a_j * b_k run on the matrix cores
     // ... or, when every one fits (kMfPPGWords), all of them in one launch before the columns,
     // grouped by a_j (mul_ppg_kernel)
@@ -236,7 +235,6 @@ bool build_plan(MulPlan &P) {
     auto new_slot = [&](int r, int64_t bound) -> uint32_t {
         const uint32_t w = bound < 0 ? 0u : slot_words(bound);
         P.slots.push_back({(uint32_t)reg[r].used, w});
-        P.slot_bound.push_back(bound);
         slot_reg.push_back((uint8_t)r);
         reg[r].used += w;
         reg[r].max = std::max(reg[r].max, reg[r].used);
@@ -483,13 +481,11 @@ bool build_plan(MulPlan &P) {
     // the MFMA spans resolved: every launch's span range of mspans, task indices relative to the
     // column's product list (ppm for the partial products' launch, prod for the carries)
     P.mrecs.assign(P.mspans.size(), MulSpanRec{});
-    auto bw = [&](uint32_t s) { return P.slot_bound[s] < 0 ? 0u : (uint32_t)(P.slot_bound[s] / 32 + 1); };
     auto resolve = [&](const MfLaunch &m, const std::vector<MulProdTask> &tasks, uint32_t t0) {
         for (uint32_t i = m.spans; i < m.spans + m.nspans; ++i) {
             const MulProdTask &t = tasks[t0 + P.mspans[i].task];
             P.mrecs[i] = MulSpanRec{P.slots[t.u].off, P.slots[t.v].off, P.slots[t.out].off,
-                                    P.slots[t.out].words, bw(t.u), bw(t.v), P.mspans[i].base, t.out,
-                                    t.u, t.v, 0u, 0u};
+                                    P.slots[t.out].words, t.u, t.v, t.out, P.mspans[i].base};
         }
     };
     for (const auto &col : P.cols) {
