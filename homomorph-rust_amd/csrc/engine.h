@@ -246,6 +246,7 @@ struct MulMfmaArgs {
     uint32_t vmax, wave_words;
     uint32_t umax;        // largest U (words; blocks of at most kMfUB): sizes the U image
     uint32_t lean;        // leaves: the lean instance (per-group U windows, 4 waves per SIMD)
+    uint32_t per_wave;    // work items per wave (set by launch_mul_mfma)
 };
 // Partial products grouped by their shared factor a_j (mul_mfma.hip mul_ppg_kernel): every
 // a_j * b_k of the plan in one launch before the columns, one wave per (value, a_j), a_j's A

@@ -156,7 +156,7 @@ __device__ __forceinline__ void mf_afrags(const uint32_t *RS, int R, int D, int 
 
 // Every tile of the span Ts .. Te - 1 that the group of G chunks from c0 reaches: two tiles at a
 // time (two accumulator chains), or (PAIRS false: 16 + 12 fewer VGPRs) one at a time
-template <int G, bool PAIRS = true, bool CONT = false, bool TRIM = false>
+template <int G, bool PAIRS = true, bool CONT = false>
 __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI, int vlo, int D,
                                          int nv, int Ts, int Te, int c0, uint32_t *OUT, MfCont &cs) {
     // tiles whose windows (words 32T - D + 2c0 .. 32T + 31 - D + 2(c0 + G) - 1) meet [0, nv)
@@ -168,30 +168,18 @@ __device__ __forceinline__ void mf_sweep(const v8i (&Af)[G], const uint32_t *VI,
         if (T <= thi) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
     } else if constexpr (CONT) {
         for (; T <= thi; ++T) mf_tile_cont<G>(Af, VI, vlo, T, Ts, c0, D, OUT, cs);
-    } else if constexpr (TRIM) {
-        // (tiny products) a tile whose windows leave V after the first ch < G chunks runs only
-        // those: the top tile of a 17 x 17-word product (33 output words) needs 1 chunk, not 9
-        for (; T <= thi; ++T) {
-            const int ch = ((nv - 1 + D - 32 * T - 2 * c0) >> 1) + 1; // chunks c0 .. c0 + ch - 1
-            switch (ch < G ? ch : 0) {
-            case 1: mf_tiles<1, 1>((const v8i(&)[1])Af, VI, vlo, T, Ts, c0, D, OUT); break;
-            case 2: mf_tiles<2, 1>((const v8i(&)[2])Af, VI, vlo, T, Ts, c0, D, OUT); break;
-            case 3: mf_tiles<3, 1>((const v8i(&)[3])Af, VI, vlo, T, Ts, c0, D, OUT); break;
-            default: mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT); break;
-            }
-        }
     } else {
         for (; T <= thi; ++T) mf_tiles<G, 1>(Af, VI, vlo, T, Ts, c0, D, OUT);
     }
 }
 
 // One group of G chunks from c0 over the tiles tlo .. thi of the span
-template <int G, bool PAIRS, bool CONT, bool TRIM = false>
+template <int G, bool PAIRS, bool CONT>
 __device__ __forceinline__ void mf_group(const uint32_t *RS, const uint32_t *VI, int vlo, int R, int D,
                                          int nv, int Ts, int Te, int c0, uint32_t *OUT, MfCont &cs) {
     v8i Af[G];
     mf_afrags<G>(RS, R, D, c0, Af);
-    mf_sweep<G, PAIRS, CONT, TRIM>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
+    mf_sweep<G, PAIRS, CONT>(Af, VI, vlo, D, nv, Ts, Te, c0, OUT, cs);
 }
 
 #ifndef HM_MF_IMG_BATCH
@@ -304,9 +292,6 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
 //    256-word leaf's LDS slice is ~9 KB instead of ~12.5 KB and 16 waves fit a CU.
 //  - wide schoolbook products (LEAF false, WIN true: U above kMfNarrowWords) the same way as the
 //    leaves: per-group U windows, spans of kMfWideLeanSpan tiles.
-#ifndef HM_MF_TRIM
-#define HM_MF_TRIM 1 // tiny instance: tiles that need fewer chunks than the group run only those
-#endif
 #ifndef HM_MFT_WPE
 #define HM_MFT_WPE 5
 #endif
@@ -318,20 +303,11 @@ __device__ __forceinline__ void mf_group_win(uint32_t wword, const uint32_t *Ub,
 #ifndef HM_MFN_GS
 #define HM_MFN_GS 16 // chunks per group of the narrow instance (A fragments held: GS + 1)
 #endif
-template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN, int GMAX = kMfG + 1, int GS = kMfG>
-__global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(GMAX <= kMfG ? HM_MFT_WPE : GS < kMfG ? HM_MFNS_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN,
-                                   GMAX <= kMfG ? HM_MFT_WPE : GS < kMfG ? HM_MFNS_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE)))
-mul_mfma_kernel(MulMfmaArgs P) {
-    extern __shared__ uint32_t lds[];
-    uint32_t *tab = lds;
-    nibble_table(tab);
-    __syncthreads();
-    const int wave = (int)rfl(threadIdx.x >> 6);
-    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    const uint64_t e = g / P.nitems;
-    if (e >= P.B.nv) return; // whole wave exits together
-    const uint32_t item = (uint32_t)(g % P.nitems);
+// One work item of mul_mfma_kernel: a leaf's whole output or one span of a schoolbook product,
+// for value e, in the wave's LDS slice (lds: the block's LDS, tab: its nibble table)
+template <bool LEAF, bool LEAN, bool WIN, int GMAX, int GS>
+__device__ __forceinline__ void mf_item(const MulMfmaArgs &P, uint64_t e, uint32_t item, uint32_t *lds,
+                                        const uint32_t *tab, int wave) {
     HM_MF_PT(tp0);
     uint32_t *arena = P.B.arena + e * P.B.astride;
     const uint32_t *U, *V, *U2 = nullptr, *V2 = nullptr;
@@ -434,7 +410,7 @@ mul_mfma_kernel(MulMfmaArgs P) {
         } else if constexpr (WIN)                                                                \
             mf_group_win<G, CONT>(ww, U + b0, ub, 0, &ww, RS, tab, VI, vlo, R, D, nv, tlo, Te, c0,  \
                                   OUTs, U2 + b0, nu2 - b0, cs);                                  \
-        else mf_group<G, !LEAN, CONT, (GMAX <= GS && HM_MF_TRIM)>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs); \
+        else mf_group<G, !LEAN, CONT>(RS, VI, vlo, R, D, nv, tlo, Te, c0, OUTs, cs);           \
         break;
             HM_MF_TAIL(1) HM_MF_TAIL(2) HM_MF_TAIL(3) HM_MF_TAIL(4) HM_MF_TAIL(5) HM_MF_TAIL(6)
             HM_MF_TAIL(7) HM_MF_TAIL(8) HM_MF_TAIL(9) HM_MF_TAIL(10) HM_MF_TAIL(11) HM_MF_TAIL(12)
@@ -462,6 +438,37 @@ mul_mfma_kernel(MulMfmaArgs P) {
         atomicAdd(&g_mf_prof[cls][4], tp9 - tp1 - t_img - t_grp); // copy-out and the rest
     }
 #endif
+}
+
+
+template <bool LEAF, bool LEAN = false, bool WIN = LEAF && LEAN, int GMAX = kMfG + 1, int GS = kMfG>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(GMAX <= kMfG ? HM_MFT_WPE : GS < kMfG ? HM_MFNS_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE_MIN,
+                                   GMAX <= kMfG ? HM_MFT_WPE : GS < kMfG ? HM_MFNS_WPE : LEAN ? HM_MFN_WPE : HM_MF_WPE)))
+mul_mfma_kernel(MulMfmaArgs P) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *tab = lds;
+    nibble_table(tab);
+    __syncthreads();
+    const int wave = (int)rfl(threadIdx.x >> 6);
+    // P.per_wave consecutive items per wave (the tiny and narrow classes: more work per wave for
+    // its nibble table, launch and LDS slice; the next item's record loads issue under this one's)
+    if constexpr (LEAF || WIN) { // (one item per wave: no loop around the big instances)
+        const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+        const uint64_t e = g / P.nitems;
+        if (e >= P.B.nv) return; // whole wave exits together
+        mf_item<LEAF, LEAN, WIN, GMAX, GS>(P, e, (uint32_t)(g % P.nitems), lds, tab, wave);
+        return;
+    }
+    const uint32_t per = P.per_wave;
+    const uint64_t g0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * per;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint64_t g = g0 + k;
+        const uint64_t e = g / P.nitems;
+        if (e >= P.B.nv) return; // whole wave exits together
+        mf_item<LEAF, LEAN, WIN, GMAX, GS>(P, e, (uint32_t)(g % P.nitems), lds, tab, wave);
+        wsync(); // (the item's last LDS reads precede the next item's writes)
+    }
 }
 
 // Partial products a_j * b_k grouped by a_j (MulPPGroup): one wave per (value, group).  a_j has
@@ -607,9 +614,16 @@ int launch_mul_ppg(const MulPPGArgs &a, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream) {
-    const uint64_t waves = a.B.nv * a.nitems;
-    if (!waves) return 0;
+#ifndef HM_MF_PER
+#define HM_MF_PER 4
+#endif
+int launch_mul_mfma(const MulMfmaArgs &args, bool leaf, void *stream) {
+    MulMfmaArgs a = args;
+    // the tiny and narrow schoolbook classes: HM_MF_PER spans per wave (their waves are short)
+    a.per_wave = (!leaf && a.umax <= kMfNarrowWords) ? HM_MF_PER : 1u; // (LEAF / WIN: 1)
+    const uint64_t items = a.B.nv * a.nitems;
+    if (!items) return 0;
+    const uint64_t waves = (items + a.per_wave - 1) / a.per_wave;
     const size_t lds = (256 + (size_t)a.wave_words * 4) * 4;
     const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
     if (leaf && a.lean)
