@@ -217,6 +217,34 @@ def time_loop(fn, steps, warmup, world, stream=None):
     return wall, ev0.elapsed_time(ev1) / 1e3
 
 
+def timed_graph(ctx, fn, reps, warmup, world=1, kernel=None):
+    """The timed region as ONE replay of a HIP graph holding `reps` steps of `fn` (the warm-up:
+    `warmup` replays of a one-step graph).  With `kernel` ("add_chain", "encrypt", "decrypt")
+    every launch of that kernel in the timed steps is timed by the engine's device wall-clock
+    stamps (hm_ctx_set_kernel_timing: one record slot per captured launch, filled by the timed
+    replay).  Returns (wall s, step s by HIP events, kernel s per launch or None, launches)."""
+    g1 = ctx.graph(fn, warmup=2)
+    for _ in range(warmup):
+        g1.replay()
+    torch.cuda.synchronize()
+    if kernel:
+        ctx.set_kernel_timing(True, kernel)
+
+    def steps():
+        for _ in range(reps):
+            fn()
+
+    gk = ctx.graph(steps, warmup=0)
+    wall, ev_s = time_loop(gk.replay, 1, 0, world)
+    ks, kn = None, 0
+    if kernel:
+        kms, kn = ctx.kernel_timing()
+        ctx.set_kernel_timing(False)
+        ks = kms / 1e3 / max(1, kn)
+    ctx.synchronize()
+    return wall, ev_s / reps, ks, kn
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -398,18 +426,16 @@ def config0_lines(device, leg_s):
     co = H.Ciphered.empty(n, ob, device, np.dtype(np.uint8))
     reps = 100
 
-    def timed(fn):
-        g = c0.graph(fn, warmup=2)
-        wall, ev_s = time_loop(g.replay, reps, 5, 1)
-        c0.synchronize()
-        return n * reps / wall, ev_s / reps
+    def timed(fn, kernel):
+        wall, step_s, ks, _ = timed_graph(c0, fn, reps, 5, 1, kernel)
+        return n * reps / wall, step_s, ks
 
-    enc_r, enc_s = timed(lambda: c0._launch(lambda: L.hm_encrypt_batch(c0._h, da.data_ptr(), 1, None,
-                                                                       ctypes.byref(cac)), "encrypt"))
-    dec_r, dec_s = timed(lambda: c0._launch(lambda: L.hm_decrypt_batch(c0._h, ctypes.byref(cac),
-                                                                       dec.data_ptr()), "decrypt"))
+    enc_r, enc_s, enc_ks = timed(lambda: c0._launch(lambda: L.hm_encrypt_batch(
+        c0._h, da.data_ptr(), 1, None, ctypes.byref(cac)), "encrypt"), "encrypt")
+    dec_r, dec_s, dec_ks = timed(lambda: c0._launch(lambda: L.hm_decrypt_batch(
+        c0._h, ctypes.byref(cac), dec.data_ptr()), "decrypt"), "decrypt")
     dec_ok = bool(np.array_equal(dec.cpu().numpy().reshape(-1), a_np))
-    add_r, add_s = timed(lambda: H.add_into(c0, ca, cb, co))
+    add_r, add_s, add_ks = timed(lambda: H.add_into(c0, ca, cb, co), "add_chain")
     got = c0.decrypt(co, np.uint8)
     add_ok = int(np.sum(got == (a_np.astype(np.uint16) + b_np).astype(np.uint8)))
     # the oracle on the same ops (its own seeded keys of the same parameters)
@@ -428,22 +454,27 @@ def config0_lines(device, leg_s):
     enc_b, dec_b = 8 * (8 * cap) + 8 * ((params[3] + 7) // 8), 8 * (8 * cap) + 1
     add_b = 2 * 8 * (8 * cap) + 8 * co.stride
     pairs = chain_bit_pairs(bound, cb.bound)
-    add_roof = mfma_roofline(2.0 * pairs * n, add_s, "add step (MFMA carry chain)",
+    add_roof = mfma_roofline(2.0 * pairs * n, add_ks, "add_chain_mfma_kernel",
                              f"{pairs} carry-product bit pairs per u8 add (static bounds), 2 ops "
-                             "per pair, over the step's HIP-event time")
-    add_roof["hbm_frac"] = add_b * n / add_s / 1e9 / HBM_PEAK_GBS
+                             "per pair, over the chain kernel's duration (device stamps of the "
+                             "timed replays)")
+    add_roof["hbm_frac"] = add_b * n / add_ks / 1e9 / HBM_PEAK_GBS
     out = {
         "config0_u8_encrypt": {
             "value": enc_r, "unit": "u8 encryptions/s", "batch": n, "params": params,
             "kernel_us_per_step": 1e6 * enc_s, "masks": "drawn per step (engine CSPRNG)",
-            "roofline": hbm_roofline(enc_b * n, enc_s, "rand_fill_kernel + encrypt_table_kernel",
-                                     f"{enc_b} algorithmic B per u8: ciphertext written, masks read"),
+            "encrypt_kernel_us": 1e6 * enc_ks,
+            "roofline": hbm_roofline(enc_b * n, enc_ks, "encrypt_table_kernel",
+                                     f"{enc_b} algorithmic B per u8: ciphertext written, masks "
+                                     "read; the encryption kernel's duration (device stamps of "
+                                     "the timed replays; the mask draw is not in it)"),
             "cpu_baseline": cpu_enc},
         "config0_u8_decrypt": {
             "value": dec_r, "unit": "u8 decryptions/s", "batch": n, "params": params,
             "verified": dec_ok, "kernel_us_per_step": 1e6 * dec_s,
-            "roofline": hbm_roofline(dec_b * n, dec_s, "decrypt_bits_kernel",
-                                     f"{dec_b} algorithmic B per u8: ciphertext read, 1 B written"),
+            "roofline": hbm_roofline(dec_b * n, dec_ks, "decrypt_bits_kernel",
+                                     f"{dec_b} algorithmic B per u8: ciphertext read, 1 B "
+                                     "written; the kernel's duration (device stamps)"),
             "cpu_baseline": cpu_dec},
         "config0_u8_add": {
             "value": add_r, "unit": "u8 homomorphic adds/s", "batch": n, "params": params,
@@ -483,23 +514,21 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
 
     reps = max(20, 5 * steps)
 
-    def timed(fn):
+    def timed(fn, kernel=None):
         # launch-bound (tens of us of kernels): replayed as one captured HIP graph per step
-        g = ctx.graph(fn, warmup=2)
-        wall, ev_s = time_loop(g.replay, reps, 2, 1)  # replays run on the current stream
-        ctx.synchronize()
-        return n * reps / wall, ev_s / reps
+        wall, step_s, ks, _ = timed_graph(ctx, fn, reps, 2, 1, kernel)
+        return n * reps / wall, step_s, ks
 
     res = {}
     for key, mp in (("csprng", None), ("predrawn", m.data_ptr())):
         dec.zero_()
-        r, ks = timed(lambda: (enc(mp), decr()))
+        r, ks, _ = timed(lambda: (enc(mp), decr()))
         res[key] = (r, bool(torch.equal(dec, data)), 1e6 * ks)
-    enc_r, enc_k = timed(lambda: enc(m.data_ptr()))
-    encc_r, encc_k = timed(lambda: enc(None))
+    enc_r, enc_k, enc_ks = timed(lambda: enc(m.data_ptr()), "encrypt")
+    encc_r, encc_k, _ = timed(lambda: enc(None))
     enc(m.data_ptr())
     dec.zero_()
-    dec_r, dec_k = timed(decr)
+    dec_r, dec_k, dec_ks = timed(decr, "decrypt")
     dec_ok = bool(torch.equal(dec, data))
     ctx.synchronize()
 
@@ -527,27 +556,31 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
                  "reference's getrandom draw is part of its encryption",
         "predrawn_masks": {"value": res["predrawn"][0], "kernel_us_per_step": res["predrawn"][2]},
         "launch": "one HIP graph replay per step (mask draw + encrypt + decrypt)",
-        "roofline": hbm_roofline(2564 * n, res["predrawn"][2] * 1e-6,
+        "roofline": hbm_roofline(2564 * n, enc_ks + dec_ks,
                                  "encrypt_table_kernel + decrypt_bits_kernel (pre-drawn masks)",
                                  "2564 algorithmic B per u32 (SURVEY.md s8(d)): 1280 B written by "
-                                 "encrypt, 1280 B read + 4 B written by decrypt; kernel time of "
-                                 "the step by HIP events"),
+                                 "encrypt, 1280 B read + 4 B written by decrypt; over the sum of "
+                                 "the two kernels' durations (device stamps in the u32_encrypt "
+                                 "and u32_decrypt_fresh legs' timed replays)"),
         "cpu_baseline": cpu_pair}
     out["u32_encrypt"] = {
         "value": encc_r, "unit": "u32 encryptions/s", "batch": n, "kernel_us_per_step": 1e6 * encc_k,
         "masks": "drawn per step (engine CSPRNG)",
-        "predrawn_masks": {"value": enc_r, "kernel_us_per_step": 1e6 * enc_k},
+        "predrawn_masks": {"value": enc_r, "kernel_us_per_step": 1e6 * enc_k,
+                           "encrypt_kernel_us": 1e6 * enc_ks},
         "readme_reference": "76.0 us per u32 on a Ryzen 7 7800X3D, 1 thread (README.md:73)",
-        "roofline": hbm_roofline(1792 * n, enc_k, "encrypt_table_kernel (pre-drawn masks)",
+        "roofline": hbm_roofline(1792 * n, enc_ks, "encrypt_table_kernel (pre-drawn masks)",
                                  "1792 algorithmic B per u32: 1280 B of ciphertext written, 512 B "
-                                 "of masks read"),
+                                 "of masks read; over the kernel's duration (device stamps of "
+                                 "the timed replays)"),
         "cpu_baseline": cpu_enc}
     out["u32_decrypt_fresh"] = {
         "value": dec_r, "unit": "u32 decryptions/s", "batch": n, "verified": dec_ok,
         "kernel_us_per_step": 1e6 * dec_k,
         "readme_reference": "12.5 us per u32 on a Ryzen 7 7800X3D, 1 thread (README.md:74)",
-        "roofline": hbm_roofline(1284 * n, dec_k, "decrypt_bits_kernel",
-                                 "1284 algorithmic B per u32: 1280 B read, 4 B written"),
+        "roofline": hbm_roofline(1284 * n, dec_ks, "decrypt_bits_kernel",
+                                 "1284 algorithmic B per u32: 1280 B read, 4 B written; over the "
+                                 "kernel's duration (device stamps of the timed replays)"),
         "cpu_baseline": cpu_dec}
     del c, dec, m
 
@@ -556,11 +589,10 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     na = add_out.n
     dbuf = torch.empty((na, 4), dtype=torch.uint8, device=device)
     ab = add_out._c()
-    g = ctx.graph(lambda: ctx._launch(lambda: L.hm_decrypt_batch(ctx._h, ctypes.byref(ab),
-                                                                 dbuf.data_ptr()), "decrypt"),
-                  warmup=2)
-    wall, ev_s = time_loop(g.replay, reps, 2, 1)
-    ctx.synchronize()
+    wall, step_s, dks, _ = timed_graph(
+        ctx, lambda: ctx._launch(lambda: L.hm_decrypt_batch(ctx._h, ctypes.byref(ab),
+                                                            dbuf.data_ptr()), "decrypt"),
+        reps, 2, 1, "decrypt")
     per_u32 = 8 * add_out.stride + 4
     ol, od = H.value_slice(add_out, 0, 4).to_host()
     cpu_dadd = oracle_leg(lambda: oracle.decrypt_batch(sk, ol, od, add_out.bound, 32, 4), 4, leg_s,
@@ -568,11 +600,12 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
                           "polynomial.rs:316-365)")
     out["u32_decrypt_after_add"] = {
         "value": na * reps / wall, "unit": "u32 decryptions/s", "batch": na,
-        "kernel_us_per_step": 1e6 * ev_s / reps,
+        "kernel_us_per_step": 1e6 * step_s,
         "readme_reference": "1.03 ms per u32 on a Ryzen 7 7800X3D, 1 thread (README.md:76)",
-        "roofline": hbm_roofline(per_u32 * na, ev_s / reps, "decrypt_kernel (wave per value)",
+        "roofline": hbm_roofline(per_u32 * na, dks, "decrypt_kernel (wave per value)",
                                  f"{per_u32} algorithmic B per u32: the add output at its static "
-                                 f"capacity read once, 4 B written"),
+                                 f"capacity read once, 4 B written; over the kernel's duration "
+                                 "(device stamps of the timed replays)"),
         "cpu_baseline": cpu_dadd}
     del dbuf
 
@@ -648,12 +681,11 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     # case of the multiply's wide outputs), one HIP graph replay per step
     d8 = torch.empty((n8, 1), dtype=torch.uint8, device=device)
     coc = co._c()
-    g8 = mctx.graph(lambda: mctx._launch(lambda: L.hm_decrypt_batch(mctx._h, ctypes.byref(coc),
-                                                                    d8.data_ptr()), "decrypt"),
-                    warmup=2)
     dreps = max(20, 5 * steps)
-    wall, ev_s = time_loop(g8.replay, dreps, 2, 1)
-    mctx.synchronize()
+    wall, step_s, dks, _ = timed_graph(
+        mctx, lambda: mctx._launch(lambda: L.hm_decrypt_batch(mctx._h, ctypes.byref(coc),
+                                                              d8.data_ptr()), "decrypt"),
+        dreps, 2, 1, "decrypt")
     per_u8 = 8 * co.stride + 1
     cpu_d8 = oracle_leg(lambda: oracle.decrypt_batch(msk, ol8, od8, co.bound, 8, 2), 2, leg_s,
                         "u8 decryptions of multiply outputs (2 per call; long division, "
@@ -661,13 +693,14 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     out["u8_decrypt_after_mul"] = {
         "value": n8 * dreps / wall, "unit": "u8 decryptions/s", "batch": n8,
         "verified": bool(np.array_equal(d8.cpu().numpy().reshape(-1), got)),
-        "kernel_us_per_step": 1e6 * ev_s / dreps,
+        "kernel_us_per_step": 1e6 * step_s,
         "reference_bench": "benches/u8.rs:31-37 (decipher after mul)",
-        "roofline": hbm_roofline(per_u8 * n8, ev_s / dreps, "decrypt_kernel (wave per value)",
+        "roofline": hbm_roofline(per_u8 * n8, dks, "decrypt_kernel (wave per value)",
                                  f"{per_u8} algorithmic B per u8: the product at its static "
-                                 f"capacity read once, 1 B written"),
+                                 f"capacity read once, 1 B written; over the kernel's duration "
+                                 "(device stamps of the timed replays)"),
         "cpu_baseline": cpu_d8}
-    del ca, cbb, co, d8, g8
+    del ca, cbb, co, d8
 
     # SURVEY.md s8 row A14, configs[3] (u32 mul, batch 1024): the first K result bits of the u32
     # carry-save circuit, bit-exact (tests: oracle fixture at K = 16, residue checks of the full
@@ -833,26 +866,23 @@ def run_add(args, world, rank, device):
     out = H.Ciphered.empty(n, ob, device, np.dtype(np.uint32))
     ctx.synchronize()
 
-    if args.graph:  # the step as one captured HIP graph (prep + chain), replayed per step
-        g = ctx.graph(lambda: H.add_into(ctx, ca, cb, out))
-        wall, ev_s = time_loop(g.replay, args.steps, args.warmup, world)
-        # a graph replay cannot carry per-launch events: the chain kernel is timed over the same
-        # number of direct launches right after the timed region
-        ctx.set_kernel_timing(True)
-        for _ in range(args.steps):
-            H.add_into(ctx, ca, cb, out)
-        chain_ms, chain_n = ctx.kernel_timing()
-        ctx.set_kernel_timing(False)
-        chain_src = f"HIP events around each chain launch on the engine stream, {chain_n} direct launches after the timed graph replays"
+    if args.graph:  # the K timed steps (prep + chain each) as one captured HIP graph
+        wall, step_s, chain_s, chain_n = timed_graph(
+            ctx, lambda: H.add_into(ctx, ca, cb, out), args.steps, args.warmup, world, "add_chain")
+        ev_s = step_s * args.steps
+        chain_src = (f"device wall-clock stamps of each of the timed region's {chain_n} chain "
+                     "launches (one replay of the K-step graph; hm_ctx_set_kernel_timing)")
     else:
         for _ in range(args.warmup):
             H.add_into(ctx, ca, cb, out)
-        ctx.set_kernel_timing(True)  # events around every chain launch of the timed region
+        ctx.set_kernel_timing(True)  # stamps of every chain launch of the timed region
         wall, ev_s = time_loop(lambda: H.add_into(ctx, ca, cb, out), args.steps, 0, world,
                                ctx.stream)
         chain_ms, chain_n = ctx.kernel_timing()
         ctx.set_kernel_timing(False)
-        chain_src = f"HIP events around each of the timed region's {chain_n} chain launches (engine stream)"
+        chain_s = chain_ms / 1e3 / max(1, chain_n)
+        chain_src = (f"device wall-clock stamps of each of the timed region's {chain_n} chain "
+                     "launches (direct launches; hm_ctx_set_kernel_timing)")
     ctx.synchronize()  # raises on any device-side error flag
     # verification (untimed): decrypt on device, gather the plaintexts over RCCL, check on rank 0
     got, wall = gather_results(world, device, ctx.decrypt_bytes(out), wall)
@@ -865,7 +895,6 @@ def run_add(args, world, rank, device):
     out_bytes = 8 * out.stride
     per_add = in_bytes + out_bytes
     kernel_s = ev_s / args.steps
-    chain_s = chain_ms / 1e3 / max(1, chain_n)
     pairs = chain_bit_pairs(ca.bound, cb.bound)
     achieved = 2.0 * pairs * n / chain_s / 1e12  # TFLOP/s: one bit-pair AND+XOR = one MAC = 2 ops
     traffic, issue = None, {}
@@ -1065,7 +1094,8 @@ def main():
     ap.add_argument("--add-pipeline", type=int, default=0,
                     help="1: big adds run as two pipelined halves; 0: one pass (engine default)")
     ap.add_argument("--graph", type=int, default=1,
-                    help="1: replay the add step as one captured HIP graph (default); 0: direct")
+                    help="1: the K timed add steps as one captured HIP graph (default); 0: direct "
+                         "launches")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "add_traffic.json"),
                     help="PMC-derived HBM bytes per add launch (scripts/traffic_json.py)")
     args = ap.parse_args()

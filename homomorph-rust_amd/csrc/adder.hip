@@ -196,10 +196,14 @@ __device__ __forceinline__ int store_sum_bit(const uint64_t *pa, uint32_t dga, c
 
 template <int WMAX, bool PAD>
 __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
+    kt_start(A.kt);
     extern __shared__ uint32_t lds[];
     const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (e >= A.n) return; // whole wave exits together
+    if (e >= A.n) { // whole wave exits together
+        kt_finish(A.kt);
+        return;
+    }
     const int lane = lane_id();
     const uint32_t L = A.nbits;
     uint32_t *Ls = lds + (size_t)wave * A.chain_lds;
@@ -237,6 +241,7 @@ __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
         offb += cap_of(A.bb.b[i]);
         offo += cap_of(A.ob.b[i]);
     }
+    kt_finish(A.kt);
 }
 
 // Staged chain (PAD plans whose slots fit in LDS).  Everything the loop reads per bit -- x_i,
@@ -245,10 +250,14 @@ __global__ void __launch_bounds__(256) add_chain_kernel(AddArgs A) {
 // only global traffic inside the loop is the output stores: no load ever waits behind them.
 template <int WMAX>
 __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
+    kt_start(A.kt);
     extern __shared__ uint32_t lds[];
     const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (e >= A.n) return; // whole wave exits together
+    if (e >= A.n) { // whole wave exits together
+        kt_finish(A.kt);
+        return;
+    }
     const int lane = lane_id();
     const uint32_t L = A.nbits;
     // LDS: [halo][C: cw][P: (L-1) cntP][AB: (L-1) cntAB][X: L cntX][degP: L][degAB: L]
@@ -283,6 +292,7 @@ __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
         }
         offo += cap_of(A.ob.b[i]);
     }
+    kt_finish(A.kt);
 }
 
 int launch_add_prep(const AddArgs &a, void *stream) {
@@ -305,15 +315,10 @@ AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n) {
     return s;
 }
 
-int launch_add(const AddArgs &a, void *stream, void *ev0, void *ev1) {
+int launch_add(const AddArgs &a, void *stream) {
     if (a.n == 0) return 0;
     if (launch_add_prep(a, stream)) return -1;
-    if (ev0 && hipEventRecord((hipEvent_t)ev0, (hipStream_t)stream) != hipSuccess) return -1;
-    int rc = 0;
-    if (a.mfma) rc = launch_add_chain_mfma(a, stream);
-    else rc = launch_add_chain_valu(a, stream);
-    if (ev1 && hipEventRecord((hipEvent_t)ev1, (hipStream_t)stream) != hipSuccess) return -1;
-    return rc;
+    return a.mfma ? launch_add_chain_mfma(a, stream) : launch_add_chain_valu(a, stream);
 }
 
 int launch_add_chain_valu(const AddArgs &a, void *stream) {

@@ -111,12 +111,17 @@ __device__ __forceinline__ void ring_put(uint32_t *ring, int w, int h, uint2 nb)
 }
 
 // Nibble images of carry words [base, base + count) into the ring (count <= 64).  Lane l writes
-// bytes 2h, 2h+1 of word base + k (k = l%32 + 32*pass, h = l/32) as two table lookups.
+// bytes 2h, 2h+1 of word base + k (k = l/2 + 32*pass, h = l%2) as two table lookups: a lane pair
+// fills one 16-byte slot, so a wave's 8-byte stores are contiguous (no LDS bank conflicts; lane
+// halves h = l/32 wrote 16-byte-strided pieces, two-way conflicted)
+#ifndef HM_RING_PAIRS
+#define HM_RING_PAIRS 1 // (A/B knob) 0: lane halves h = l/32 fill the slots' halves
+#endif
 template <int kMirror>
 __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, const uint32_t *tab,
                                           int base, int count, int lane) {
-    const int h = lane >> 5;
-    for (int k = lane & 31; k < count; k += 32) {
+    const int h = HM_RING_PAIRS ? lane & 1 : lane >> 5;
+    for (int k = HM_RING_PAIRS ? lane >> 1 : lane & 31; k < count; k += 32) {
         const int w = base + k;
         const uint32_t v = C[w] >> (16 * h);
         uint2 nb;
@@ -139,6 +144,7 @@ template <int NC>
 __global__ void __launch_bounds__(64 * kMfmaWpb)
 __attribute__((amdgpu_waves_per_eu(MfmaCfg<NC>::kWavesPerEU, MfmaCfg<NC>::kWavesPerEU)))
 add_chain_mfma_kernel(AddArgs A) {
+    kt_start(A.kt);
     using Cfg = MfmaCfg<NC>;
     constexpr int kRevWords = Cfg::kRevWords, kRsWords = Cfg::kRsWords, kRec = Cfg::kRecWords;
     extern __shared__ uint32_t lds[];
@@ -153,7 +159,10 @@ add_chain_mfma_kernel(AddArgs A) {
     __syncthreads();
     const int wave = (int)rfl(threadIdx.x >> 6); // wave-uniform by construction
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (e >= A.n) return; // whole wave exits together
+    if (e >= A.n) { // whole wave exits together
+        kt_finish(A.kt);
+        return;
+    }
     const int lane = lane_id();
     const uint32_t L = A.nbits;
     // LDS per wave: [halo][C: mf_cw][ring: kRingWords][RS: kRsWords]
@@ -336,7 +345,9 @@ add_chain_mfma_kernel(AddArgs A) {
             // (tile 0 stages words -32-D+col too: its ring slots are outside tile 0's window, C
             // reads below the halo stay inside the block's LDS, and the next bit refills its window
             // before reading it, so no per-tile test is needed)
-            const int fw = 32 * (T - 1) - D + col;
+            // (lane pair 2j, 2j + 1: word j's two halves, contiguous stores as in ring_fill)
+            const int fh = HM_RING_PAIRS ? lane & 1 : h;
+            const int fw = 32 * (T - 1) - D + (HM_RING_PAIRS ? lane >> 1 : col);
             uint32_t fv;
             uint2 fn;
             // ab_i's word of this tile's output, read before the MFMAs (ab_i < 64 words: host plan;
@@ -354,11 +365,11 @@ add_chain_mfma_kernel(AddArgs A) {
                 if (stage == 0) fv = C[fw];
                 else if (stage == 1) {
                     asm volatile("" : "+v"(fv));
-                    fv >>= 16 * h;
+                    fv >>= 16 * fh;
                     fn.x = tab[fv & 0xFFu], fn.y = tab[(fv >> 8) & 0xFFu];
                 } else {
                     asm volatile("" : "+v"(fn.x), "+v"(fn.y));
-                    ring_put<Cfg::kMirror>(ring, fw, h, fn);
+                    ring_put<Cfg::kMirror>(ring, fw, fh, fn);
                 }
             });
             __builtin_amdgcn_s_setprio(0);
@@ -404,6 +415,7 @@ add_chain_mfma_kernel(AddArgs A) {
     if (lane == 0)
         for (int k = 0; k < 4; ++k) g_mfma_prof[e * 4 + k] = prof[k];
 #endif
+    kt_finish(A.kt);
 }
 
 int launch_add_chain_mfma(const AddArgs &a, void *stream) {

@@ -333,10 +333,9 @@ void hm_ctx_destroy(hm_ctx *c) try {
     mul_plans_release(c);
     for (void *p : {(void *)c->d_pk, (void *)c->d_pk_tab, (void *)c->d_pk_tab1, (void *)c->d_s,
                     (void *)c->d_ws_add, (void *)c->d_status, (void *)c->d_nonce,
-                    (void *)c->d_masks, (void *)c->d_mws})
+                    (void *)c->d_masks, (void *)c->d_mws, (void *)c->d_kt})
         if (p) (void)hipFree(p);
     for (auto &r : c->retired) (void)hipFree(r.p);
-    for (auto &e : c->tev) (void)hipEventDestroy(e);
     for (hipEvent_t e : {c->ev_fork, c->ev_mid, c->ev_join})
         if (e) (void)hipEventDestroy(e);
     if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
@@ -483,37 +482,50 @@ hm_status hm_ctx_get_public_key(const hm_ctx *c, uint64_t *limbs, size_t cap, ui
 } HM_ABI_CATCH
 
 hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) try {
-    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (!c || enable < HM_TIME_OFF || enable > HM_TIME_DECRYPT) return HM_ERR_INVALID_ARGUMENT;
     DeviceGuard g(c->device);
-    if (enable && c->tev.empty()) {
-        // created into a local vector and kept only when every event exists
-        std::vector<hipEvent_t> ev(2 * kTimedLaunches, nullptr);
-        for (size_t k = 0; k < ev.size(); ++k) {
-            const hipError_t e = hipEventCreate(&ev[k]);
-            if (e != hipSuccess) {
-                for (size_t j = 0; j < k; ++j) (void)hipEventDestroy(ev[j]);
-                return hip_fail(c, e);
-            }
-        }
-        c->tev.swap(ev);
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    const size_t half = (size_t)kTimedLaunches * kTimerWaves * sizeof(unsigned long long);
+    if (enable && !c->d_kt) {
+        void *p = nullptr;
+        HM_HIP(c, hipMalloc(&p, 2 * half));
+        c->d_kt = (unsigned long long *)p;
     }
-    c->time_chain = enable != 0;
-    c->tev_used = 0;
+    if (c->d_kt) { // reset: starts at the maximum (atomic min), ends at 0 (atomic max)
+        HM_HIP(c, hipMemset(c->d_kt, 0xFF, half));
+        HM_HIP(c, hipMemset((char *)c->d_kt + half, 0, half));
+    }
+    c->time_kernel = (uint32_t)enable;
+    c->kt_next = 0;
     return HM_OK;
 } HM_ABI_CATCH
 
 hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) try {
     if (!c || !total_ms || !launches) return HM_ERR_INVALID_ARGUMENT;
+    *total_ms = 0.0, *launches = 0;
+    if (!c->d_kt || !c->kt_next) return HM_OK;
     DeviceGuard g(c->device);
     HM_HIP(c, hipStreamSynchronize(c->stream));
-    double t = 0.0;
-    for (size_t k = 0; k + 1 < c->tev_used; k += 2) {
-        float ms = 0.0f;
-        HM_HIP(c, hipEventElapsedTime(&ms, c->tev[k], c->tev[k + 1]));
-        t += ms;
+    const size_t n = (size_t)c->kt_next * kTimerWaves;
+    std::vector<unsigned long long> t0(n), t1(n);
+    HM_HIP(c, hipMemcpy(t0.data(), c->d_kt, n * 8, hipMemcpyDeviceToHost));
+    HM_HIP(c, hipMemcpy(t1.data(), c->d_kt + (size_t)kTimedLaunches * kTimerWaves, n * 8,
+                        hipMemcpyDeviceToHost));
+    int rate_khz = 0; // the wall clock's frequency (100 MHz on gfx9)
+    HM_HIP(c, hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->device));
+    if (rate_khz <= 0) return HM_ERR_UNSUPPORTED;
+    double ticks = 0.0;
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < c->kt_next; ++s) {
+        unsigned long long lo = ~0ull, hi = 0ull;
+        for (size_t w = (size_t)s * kTimerWaves; w < (size_t)(s + 1) * kTimerWaves; ++w)
+            lo = std::min(lo, t0[w]), hi = std::max(hi, t1[w]);
+        if (lo == ~0ull || hi < lo) continue; // (a slot whose launch has not run)
+        ticks += (double)(hi - lo);
+        ++k;
     }
-    *total_ms = t;
-    *launches = (uint32_t)(c->tev_used / 2);
+    *total_ms = ticks / rate_khz;
+    *launches = k;
     return HM_OK;
 } HM_ABI_CATCH
 
@@ -682,6 +694,7 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
         E.nonce_bump = c->d_nonce;
     }
     E.masks = masks;
+    E.kt = c->ktimer(HM_TIME_ENCRYPT);
     int r = launch_encrypt(E, c->stream);
     if (r == HM_ERR_UNSUPPORTED) return HM_ERR_UNSUPPORTED;
     return r ? hip_fail(c, hipGetLastError()) : HM_OK;
@@ -718,6 +731,7 @@ hm_status hm_decrypt_batch(hm_ctx *c, const hm_batch *in, uint8_t *out) try {
     D.ucap = cap_of(in->bound[0]) <= 8 ? cap_of(in->bound[0]) : 0;
     for (uint32_t i = 1; i < in->nbits; ++i)
         if (cap_of(in->bound[i]) != D.ucap) D.ucap = 0;
+    D.kt = c->ktimer(HM_TIME_DECRYPT);
     DeviceGuard g(c->device);
     return launch_decrypt(D, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 } HM_ABI_CATCH
@@ -825,21 +839,13 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     A.n = a->n, A.nbits = L;
     A.status = c->d_status;
     fill_bounds(A.ab, a), fill_bounds(A.bb, b), fill_bounds(A.ob, out);
-    void *ev[2] = {nullptr, nullptr};
-    if (c->time_chain) {
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        (void)hipStreamIsCapturing(c->stream, &cap);
-        if (cap == hipStreamCaptureStatusNone && c->tev_used + 2 <= c->tev.size()) {
-            ev[0] = c->tev[c->tev_used], ev[1] = c->tev[c->tev_used + 1];
-            c->tev_used += 2;
-        }
-    }
+    A.kt = c->ktimer(HM_TIME_ADD_CHAIN);
     // Two-stage pipeline (not while timing the chain): the batch in two halves, the second
     // half's prep on the auxiliary stream right after the first half's, so it runs beside the
     // first half's chain (the chain is matrix-core and latency bound, the prep VALU bound); the
     // halves use disjoint workspace and outputs.  Fork / join by events, so a graph captured on
     // the context stream holds both branches.
-    if (c->add_pipe && !c->time_chain && A.mfma && a->n >= 2 * kAddPipeMin) {
+    if (c->add_pipe && !A.kt.t0 && A.mfma && a->n >= 2 * kAddPipeMin) {
         if (hm_status st = ensure_aux_stream(c); st) return st;
         const uint64_t h = (a->n / 2 + kAddWavesPerBlock - 1) / kAddWavesPerBlock * kAddWavesPerBlock;
         const AddArgs A1 = add_args_slice(A, 0, h), A2 = add_args_slice(A, h, a->n - h);
@@ -855,7 +861,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         HM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
         return HM_OK;
     }
-    return launch_add(A, c->stream, ev[0], ev[1]) ? hip_fail(c, hipGetLastError()) : HM_OK;
+    return launch_add(A, c->stream) ? hip_fail(c, hipGetLastError()) : HM_OK;
 } HM_ABI_CATCH
 
 hm_status hm_mul_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, int is_signed,
@@ -1038,5 +1044,7 @@ hm_status hm_ctx_synchronize(hm_ctx *c) try {
     }
     return (hm_status)st;
 } HM_ABI_CATCH
+
+int32_t hm_ctx_last_hip_error(const hm_ctx *c) { return c ? (int32_t)c->last_hip : 0; }
 
 } // extern "C"

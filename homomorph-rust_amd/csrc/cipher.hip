@@ -24,10 +24,14 @@ __device__ __forceinline__ void enc_nonce_bump(const EncArgs &E) {
 
 template <int PC>
 __global__ void __launch_bounds__(256) encrypt_kernel(EncArgs E) {
+    kt_start(E.kt);
     enc_nonce_bump(E);
     const uint32_t nbits = E.nbytes * 8;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= E.n * nbits) return;
+    if (t >= E.n * nbits) {
+        kt_finish(E.kt);
+        return;
+    }
     const uint64_t e = t / nbits;
     const uint32_t k = (uint32_t)(t % nbits);
     const uint32_t mb = (E.tau + 7) / 8;
@@ -70,6 +74,7 @@ __global__ void __launch_bounds__(256) encrypt_kernel(EncArgs E) {
     for (uint32_t l = PC; l < cap; ++l) dst[l] = 0ull;
     if ((uint32_t)deg > E.ob.b[k]) flag(E.status, HM_ERR_CAPACITY);
     E.out.degree[e * nbits + k] = (uint32_t)deg;
+    kt_finish(E.kt);
 }
 
 // Table form of the same subset sum (four Russians over the mask): the public-key rows are taken
@@ -233,6 +238,7 @@ __device__ __forceinline__ void enc_table_to_lds(const uint64_t *ptab, uint32_t 
 template <int PC, int GC, bool TOP1 = false>
 __global__ void __launch_bounds__(kEncBlock) __attribute__((amdgpu_waves_per_eu(HM_ENC_TAB_WPE)))
 encrypt_table_kernel(EncArgs E) {
+    kt_start(E.kt);
     enc_nonce_bump(E);
     constexpr int NP = kEncTabPairs<PC, TOP1>; // limb pairs (TOP1: the table without the top limb)
     extern __shared__ uint64_t tab[];          // [G][NP][16][2] (upload_pk)
@@ -285,6 +291,7 @@ encrypt_table_kernel(EncArgs E) {
             enc_finish<PC>(E, acc, st, t0, total, live, e, k, nbits);
         }
     }
+    kt_finish(E.kt);
 }
 
 // ChaCha20 block blk of (key, nonce) (D. J. Bernstein's original layout: constants, 256-bit key,
@@ -387,59 +394,63 @@ int launch_encrypt(const EncArgs &E, void *stream) {
 
 // ---------------------------------------------------------------------------------------------
 // Decryption: bit = parity(C & z) with z_k = (X^k mod S)(0).  Wide ciphertexts (circuit outputs):
-// one wavefront per value; lanes stride over the value's limbs (coalesced), accumulate per-bit
-// parities, XOR-reduce.  Limbs go kDecUnroll per lane at a time: their bits and z indices first
-// (ALU only), then all their limb and z loads together, so each lane has 2 kDecUnroll loads in
-// flight instead of one dependent pair.
-constexpr uint32_t kDecUnroll = 8;
+// one wavefront per value.  The bits are walked in a uniform loop; the lanes stride over the bit's
+// limbs (contiguous, so the loads coalesce) with kDecUnroll independent accumulators (that many
+// limb + z load pairs in flight per lane), and the bit is the parity of the ballot of the lanes'
+// parities.  No lane-dependent control flow besides the strided bounds: every lane runs the same
+// bit loop (an earlier form walked a per-lane bit cursor through the flattened limbs; its
+// data-dependent inner loops compiled into a schedule that read some limbs wrongly once an
+// unrelated argument field was added -- kept out of the way of such codegen).
+constexpr uint32_t kDecUnroll = 4;
+static_assert(kDecUnroll == 4, "the accumulator fold below names four");
 __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
+    kt_start(D.kt);
     const int wave = (int)rfl(threadIdx.x >> 6);
     const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (e >= D.n) return;
-    const int lane = lane_id();
-    const uint64_t *src = D.in.limbs + e * D.in.stride;
-    const uint32_t total = (uint32_t)D.in.stride;
-    uint64_t m0 = 0, m1 = 0;
-    // bit i of the value owns limbs [lo, hi); each lane walks its limbs in increasing order
-    uint32_t i = 0, lo = 0, hi = cap_of(D.ib.b[0]);
-    bool bad = false;
-    for (uint32_t g0 = lane; g0 < total; g0 += kDecUnroll * kWave) {
-        uint32_t bi[kDecUnroll], zi[kDecUnroll];
+    if (e < D.n) { // whole wave together
+        const uint32_t lane = (uint32_t)lane_id();
+        const uint64_t *src = D.in.limbs + e * D.in.stride;
+        uint64_t m0 = 0, m1 = 0; // plaintext bits 0..63, 64..127 (wave-uniform)
+        bool bad = false;
+        for (uint32_t i = 0; i < D.nbits; ++i) {
+            const uint32_t cap = cap_of(D.ib.b[i]);
+            const uint64_t *p = src + D.ioff.b[i];
+            uint64_t acc[kDecUnroll];
 #pragma unroll
-        for (uint32_t u = 0; u < kDecUnroll; ++u) {
-            const uint32_t g = g0 + u * kWave;
-            if (g < total)
-                while (g >= hi) {
-                    ++i;
-                    lo = hi;
-                    hi += cap_of(D.ib.b[i]);
+            for (uint32_t u = 0; u < kDecUnroll; ++u) acc[u] = 0;
+            uint32_t k = lane;
+            for (; k + (kDecUnroll - 1) * kWave < cap; k += kDecUnroll * kWave) {
+                uint64_t v[kDecUnroll], z[kDecUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kDecUnroll; ++u) v[u] = p[k + u * kWave];
+#pragma unroll
+                for (uint32_t u = 0; u < kDecUnroll; ++u) {
+                    const uint32_t kz = k + u * kWave;
+                    z[u] = kz < D.zlimbs ? D.z[kz] : 0ull;
+                    bad |= kz >= D.zlimbs && v[u] != 0;
                 }
-            bi[u] = i, zi[u] = g - lo;
-        }
-        uint64_t v[kDecUnroll], z[kDecUnroll];
 #pragma unroll
-        for (uint32_t u = 0; u < kDecUnroll; ++u) {
-            const uint32_t g = g0 + u * kWave;
-            v[u] = g < total ? src[g] : 0ull;
-            z[u] = zi[u] < D.zlimbs ? D.z[zi[u]] : 0ull;
+                for (uint32_t u = 0; u < kDecUnroll; ++u) acc[u] ^= v[u] & z[u];
+            }
+            for (; k < cap; k += kWave) {
+                const uint64_t v = p[k];
+                acc[0] ^= v & (k < D.zlimbs ? D.z[k] : 0ull);
+                bad |= k >= D.zlimbs && v != 0;
+            }
+            const uint64_t a = (acc[0] ^ acc[1]) ^ (acc[2] ^ acc[3]);
+            const uint64_t par = __ballot(__builtin_popcountll(a) & 1);
+            const uint64_t bit = (uint64_t)(__builtin_popcountll(par) & 1);
+            if (i < 64) m0 |= bit << i;
+            else m1 |= bit << (i - 64);
         }
-#pragma unroll
-        for (uint32_t u = 0; u < kDecUnroll; ++u) {
-            if (zi[u] >= D.zlimbs && v[u]) bad = true;
-            const uint64_t p = (uint64_t)(__builtin_popcountll(v[u] & z[u]) & 1);
-            if (bi[u] < 64) m0 ^= p << bi[u];
-            else m1 ^= p << (bi[u] - 64);
+        if (__any(bad) && lane == 0) flag(D.status, HM_ERR_UNSUPPORTED);
+        const uint32_t nbytes = D.nbits / 8;
+        if (lane < nbytes) {
+            const uint64_t w = lane < 8 ? m0 : m1;
+            D.out[e * nbytes + lane] = (uint8_t)(w >> (8 * (lane & 7)));
         }
     }
-    if (__any(bad) && lane == 0) flag(D.status, HM_ERR_UNSUPPORTED);
-    const uint32_t r0 = wave_xor_u32((uint32_t)m0), r1 = wave_xor_u32((uint32_t)(m0 >> 32));
-    const uint32_t r2 = wave_xor_u32((uint32_t)m1), r3 = wave_xor_u32((uint32_t)(m1 >> 32));
-    const uint32_t nbytes = D.nbits / 8;
-    if ((uint32_t)lane < nbytes) {
-        const uint32_t w = lane / 4;
-        const uint32_t word = w == 0 ? r0 : w == 1 ? r1 : w == 2 ? r2 : r3;
-        D.out[e * nbytes + lane] = (uint8_t)(word >> (8 * (lane % 4)));
-    }
+    kt_finish(D.kt);
 }
 
 // Narrow ciphertexts (fresh ones: 5 limbs at d+dp = 256): one lane per ciphertext bit.  A lane
@@ -448,6 +459,7 @@ __global__ void __launch_bounds__(256) decrypt_kernel(DecArgs D) {
 // nbits = 8 nbytes), so one ballot gives 8 output bytes.  Lanes read consecutive polynomials:
 // the loads stream the batch once.
 __global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
+    kt_start(D.kt);
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t total = D.n * D.nbits;
     uint32_t p = 0;
@@ -488,6 +500,7 @@ __global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
             for (uint64_t b = 0; b < 8 && g0 + 8 * b < total; ++b) dst[b] = (uint8_t)(bits >> (8 * b));
         }
     }
+    kt_finish(D.kt);
 }
 
 int launch_decrypt(const DecArgs &D, void *stream) {

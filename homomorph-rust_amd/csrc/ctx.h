@@ -84,11 +84,17 @@ struct hm_ctx {
     bool add_pipe = false;
     hipStream_t aux_stream = nullptr;  // created on first use
     hipEvent_t ev_fork = nullptr, ev_mid = nullptr, ev_join = nullptr;
-    // per-launch timing of the adder's carry-chain kernel (hm_ctx_set_kernel_timing): a pair of
-    // HIP events recorded around each chain launch on the engine stream
-    bool time_chain = false;
-    std::vector<hipEvent_t> tev; // 2 per recorded launch
-    size_t tev_used = 0;
+    // per-launch timing of one kernel (hm_ctx_set_kernel_timing, HM_TIME_*): device wall-clock
+    // stamps (engine.h KTimer) in d_kt: [kTimedLaunches][kTimerWaves] starts, then as many ends;
+    // kt_next = the next launch's slot
+    uint32_t time_kernel = HM_TIME_OFF;
+    unsigned long long *d_kt = nullptr;
+    uint32_t kt_next = 0;
+    hm::KTimer ktimer(uint32_t which) {
+        if (time_kernel != which || !d_kt || kt_next >= hm::kTimedLaunches) return hm::KTimer{nullptr, nullptr};
+        const size_t slot = (size_t)kt_next++ * hm::kTimerWaves;
+        return hm::KTimer{d_kt + slot, d_kt + (size_t)hm::kTimedLaunches * hm::kTimerWaves + slot};
+    }
 };
 
 namespace hm {

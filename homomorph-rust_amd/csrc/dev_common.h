@@ -248,6 +248,24 @@ __device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__rest
     }
 }
 
+// Kernel timer (engine.h KTimer): lane 0 of every wave stamps the device wall clock (100 MHz)
+// at the kernel's entry and at its exit.  Fire-and-forget atomics on per-wave addresses: no
+// barrier, no LDS, no contention (an earlier form counted blocks out on one global counter with
+// a static LDS word; the LDS word misaligned the kernels' dynamic LDS and the counter serialised).
+__device__ __forceinline__ uint32_t kt_wave() {
+    return (blockIdx.x * ((blockDim.x + 63u) >> 6) + (threadIdx.x >> 6)) & (kTimerWaves - 1);
+}
+__device__ __forceinline__ void kt_start(const KTimer &k) {
+    if (k.t0 && (threadIdx.x & 63u) == 0)
+        __hip_atomic_fetch_min(&k.t0[kt_wave()], (unsigned long long)wall_clock64(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void kt_finish(const KTimer &k) {
+    if (k.t1 && (threadIdx.x & 63u) == 0)
+        __hip_atomic_fetch_max(&k.t1[kt_wave()], (unsigned long long)wall_clock64(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ int bitwords(int degp1) { return degp1 ? ((degp1 - 1) >> 5) + 1 : 0; }
 
 } // namespace hm

@@ -13,6 +13,16 @@ struct Bounds {
     uint32_t b[HM_MAX_BITS];
 };
 
+// Kernel timer (hm_ctx_set_kernel_timing): device wall-clock stamps of one launch, in the slot
+// the host gave it (one slot per launch made or captured while timing is on, so every launch of a
+// captured K-step graph has its own).  Each wave's lane 0 stamps its start into t0[w] and its end
+// into t1[w] (w = the wave's index in the grid, modulo kTimerWaves; relaxed min / max atomics on
+// distinct addresses, nothing waits on them); the host takes the slot's earliest start and latest end.
+struct KTimer {
+    unsigned long long *t0; // null: timing off
+    unsigned long long *t1;
+};
+
 struct BatchArg {
     uint64_t *limbs;
     uint32_t *degree;
@@ -45,6 +55,7 @@ struct AddArgs {
     uint32_t mf_cw;                   // MFMA chain: carry bit words (tiles, window overhang)
     int *status;
     Bounds ab, bb, ob;
+    KTimer kt; // the carry-chain kernel's launches
 };
 
 struct EncArgs {
@@ -68,6 +79,7 @@ struct EncArgs {
     uint32_t top1;
     uint32_t topcol[4];
     uint64_t *nonce_bump; // non-null: advance this CSPRNG nonce (the masks were just drawn)
+    KTimer kt;
 };
 
 struct DecArgs {
@@ -82,6 +94,7 @@ struct DecArgs {
     Bounds ioff;     // limb offset of each bit within a value (prefix sums of the caps)
     uint32_t maxcap; // widest bit (limbs): picks lane-per-bit or wave-per-value
     uint32_t ucap;   // every bit has exactly ucap <= 8 limbs (fresh ciphertexts), else 0
+    KTimer kt;
 };
 
 // Gates keep their intermediates in LDS, one wavefront per value.
@@ -319,7 +332,7 @@ struct RandArgs {
 // bump false: the nonce is left for the caller's next launch to advance (EncArgs::nonce_bump)
 int launch_random(const RandArgs &a, void *stream, bool bump = true);
 // ev0/ev1 (hipEvent_t, may be null): recorded on the stream around the carry-chain launch
-int launch_add(const AddArgs &a, void *stream, void *ev0 = nullptr, void *ev1 = nullptr);
+int launch_add(const AddArgs &a, void *stream);
 int launch_add_prep(const AddArgs &a, void *stream);
 // the same add over values [e0, e0 + n) of a batch: argument block with every pointer advanced
 AddArgs add_args_slice(const AddArgs &a, uint64_t e0, uint64_t n);
@@ -355,7 +368,8 @@ int launch_poly_rem(const PolyArgs &a, const RemTable &t, void *stream);
 
 constexpr int kAddWavesPerBlock = 4;
 constexpr uint64_t kAddPipeMin = 1024; // values per half of a pipelined add (hm_ctx_set_add_pipeline)
-constexpr size_t kTimedLaunches = 4096; // chain launches hm_ctx_set_kernel_timing can record
+constexpr uint32_t kTimedLaunches = 128;  // launches hm_ctx_set_kernel_timing can record
+constexpr uint32_t kTimerWaves = 32768;   // stamp pairs per launch (waves beyond share them)
 // MFMA carry chain (adder_mfma.hip), one configuration per chunk count NC: P_i within 2 NC - 1
 // words (NC = 13: 25 words, d + d' <= 256; NC = 25: 49 words, d + d' <= 512), nibble ring slots
 // (a power of two above a tile's 32 + 2 NC word window plus the 32 words filled ahead), zero carry

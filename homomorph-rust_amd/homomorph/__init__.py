@@ -400,12 +400,18 @@ class Context:
     def _launch(self, fn, what: str):
         torch = _torch()
         if torch.cuda.is_current_stream_capturing():
-            _check(fn(), what)  # inside Context.graph: the engine stream is the capture stream
+            # inside Context.graph: the engine stream is the capture stream
+            self._check_hip(fn(), what)
             return
         cur = torch.cuda.current_stream(self.device)
         self._stream.wait_stream(cur)
         st = fn()
         cur.wait_stream(self._stream)
+        self._check_hip(st, what)
+
+    def _check_hip(self, st: int, what: str):
+        if st == _lib.ERR_HIP:  # name the runtime's own code (hm_ctx_last_hip_error)
+            what = f"{what} (hipError_t {lib().hm_ctx_last_hip_error(self._h)})"
         _check(st, what)
 
     def graph(self, fn, warmup: int = 1) -> "EngineGraph":
@@ -446,13 +452,18 @@ class Context:
         either way."""
         _check(lib().hm_ctx_set_add_pipeline(self._h, int(bool(enable))), "hm_ctx_set_add_pipeline")
 
-    def set_kernel_timing(self, enable: bool = True):
-        """hm_ctx_set_kernel_timing: record HIP events around every carry-chain launch of the
-        adder (outside graph capture) from now on; kernel_timing() reads them back."""
-        _check(lib().hm_ctx_set_kernel_timing(self._h, int(bool(enable))), "hm_ctx_set_kernel_timing")
+    TIMED_KERNELS = {"add_chain": 1, "encrypt": 2, "decrypt": 3}
+
+    def set_kernel_timing(self, enable: bool = True, kernel: str = "add_chain"):
+        """hm_ctx_set_kernel_timing: time the launches of `kernel` ("add_chain": the adder's
+        carry chain, "encrypt", "decrypt") made or captured from now on (one record slot each,
+        up to 128; a captured launch's slot holds its last replay) by device wall-clock stamps;
+        kernel_timing() reads them back.  Resets the record."""
+        k = self.TIMED_KERNELS[kernel] if enable else 0
+        _check(lib().hm_ctx_set_kernel_timing(self._h, k), "hm_ctx_set_kernel_timing")
 
     def kernel_timing(self):
-        """(summed carry-chain kernel ms, launches) since set_kernel_timing(True)."""
+        """(summed kernel ms, launches) of the timed kernel since set_kernel_timing."""
         t = ctypes.c_double(0.0)
         n = ctypes.c_uint32(0)
         _check(lib().hm_ctx_kernel_timing(self._h, ctypes.byref(t), ctypes.byref(n)),

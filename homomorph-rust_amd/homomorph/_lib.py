@@ -106,6 +106,7 @@ SIGNATURES = {
     "hm_wire_encode": (ctypes.c_int, [vp, ctypes.POINTER(HmBatch), vp, ctypes.c_size_t]),
     "hm_wire_decode": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.POINTER(HmBatch)]),
     "hm_ctx_synchronize": (ctypes.c_int, [vp]),
+    "hm_ctx_last_hip_error": (ctypes.c_int32, [vp]),
 }
 
 _lib = None

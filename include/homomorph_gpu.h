@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 3
+#define HM_ABI_VERSION 4 /* 4: kernel timing by device stamps (HM_TIME_*), hm_ctx_last_hip_error */
 #define HM_MAX_BITS 128 /* u128 is the widest type with impls (src/impls/numbers/uint.rs:58) */
 
 typedef enum hm_status {
@@ -191,12 +191,19 @@ hm_status hm_ctx_set_add_options(hm_ctx *ctx, uint32_t chain);
  * holds both branches).  Not used while kernel timing is on. */
 hm_status hm_ctx_set_add_pipeline(hm_ctx *ctx, int enable);
 
-/* Kernel timing (measurement only; no effect on results).  While enabled, every hm_add_batch
- * outside a stream capture records a pair of HIP events on the engine stream around its
- * carry-chain kernel (the dominant kernel of the add), up to 4096 launches; enabling resets the
- * record.  hm_ctx_kernel_timing synchronizes the stream and returns the summed chain time and the
- * number of launches recorded. */
-hm_status hm_ctx_set_kernel_timing(hm_ctx *ctx, int enable);
+/* Kernel timing (measurement only; no effect on results).  hm_ctx_set_kernel_timing(ctx, k)
+ * times kernel k from now on (HM_TIME_OFF stops; setting resets the record and synchronizes the
+ * stream): every launch of it made -- or captured into a graph -- while timing is on takes its
+ * own record slot (up to 128), in which the kernel's waves stamp the device wall clock at their
+ * start and end.  A captured launch's slot is refilled by every replay of its graph (the last
+ * replay's stamps remain), so a K-step graph replayed once yields K launches.
+ * hm_ctx_kernel_timing synchronizes the stream and returns the summed duration (earliest wave
+ * start to latest wave end, per slot) of the launches recorded and their number.
+ * HM_TIME_ADD_CHAIN = 1 (hm_add_batch's carry chain, the dominant kernel of the add),
+ * HM_TIME_ENCRYPT: hm_encrypt_batch's encryption kernel (not the mask draw), HM_TIME_DECRYPT:
+ * hm_decrypt_batch's kernel. */
+enum { HM_TIME_OFF = 0, HM_TIME_ADD_CHAIN = 1, HM_TIME_ENCRYPT = 2, HM_TIME_DECRYPT = 3 };
+hm_status hm_ctx_set_kernel_timing(hm_ctx *ctx, int kernel);
 hm_status hm_ctx_kernel_timing(hm_ctx *ctx, double *total_ms, uint32_t *launches);
 
 /* Context::validate_operation (src/context.rs:310-323): HM_OK or HM_ERR_INVALID_PARAMETERS with
@@ -322,6 +329,9 @@ hm_status hm_wire_decode(hm_ctx *ctx, const uint8_t *src, size_t len, hm_batch *
 /* Waits for the context's stream, then returns (and clears) the first device-side error raised by
  * any kernel since the last check (HM_ERR_CAPACITY, HM_ERR_BAD_INPUT) or a HIP error. */
 hm_status hm_ctx_synchronize(hm_ctx *ctx);
+/* The HIP runtime's error code (hipError_t) behind the context's most recent HM_ERR_HIP, or 0;
+ * diagnostic only, not cleared by this call (hm_ctx_synchronize clears it). */
+int32_t hm_ctx_last_hip_error(const hm_ctx *ctx);
 
 #ifdef __cplusplus
 }

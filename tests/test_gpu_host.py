@@ -180,3 +180,46 @@ def test_apply1_is_in_place_and_apply_n_runs_user_ops(H, oracle):
 
     with pytest.raises(H.OperationError):
         ctx.apply_n(Needy, [c, c, c])
+
+
+def test_kernel_timing_counts_direct_and_graph_launches(H):
+    """hm_ctx_set_kernel_timing: every launch of the selected kernel is stamped on the device,
+    direct launches and launches captured into a graph alike (the bench times one replay of a
+    K-step graph this way), and a launch's duration fits inside the event-timed steps around it."""
+    import torch
+    ctx = H.Context(H.Parameters(128, 128, 1, 128))
+    ctx.seed_rng(77)
+    ctx.generate_secret_key()
+    ctx.generate_public_key()
+    a = np.arange(256, dtype=np.uint32) * np.uint32(2654435761)  # wraps mod 2^32
+    ca, cb = ctx.encrypt(a.astype(np.uint32)), ctx.encrypt((a ^ 0xFFFF).astype(np.uint32))
+    out = H.Ciphered.empty(256, H.add_out_bounds(ca.bound, cb.bound), "cuda:0", np.dtype(np.uint32))
+    H.add_into(ctx, ca, cb, out)
+    ctx.set_kernel_timing(True, "add_chain")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(ctx.stream)
+    for _ in range(3):
+        H.add_into(ctx, ca, cb, out)
+    ev1.record(ctx.stream)
+    ms, n = ctx.kernel_timing()
+    torch.cuda.synchronize()
+    assert n == 3 and 0 < ms < ev0.elapsed_time(ev1)
+    ctx.set_kernel_timing(True, "add_chain")  # reset
+    # three launches captured into one graph: three record slots, refilled by every replay
+    g = ctx.graph(lambda: [H.add_into(ctx, ca, cb, out) for _ in range(3)], warmup=0)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    ms, n = ctx.kernel_timing()
+    assert n == 3 and ms > 0
+    got = ctx.decrypt(out, np.uint32)
+    assert np.array_equal(got, (a + (a ^ 0xFFFF)).astype(np.uint32))
+    ctx.set_kernel_timing(True, "encrypt")
+    c = ctx.encrypt(a)
+    assert ctx.kernel_timing()[1] == 1
+    ctx.set_kernel_timing(True, "decrypt")
+    assert np.array_equal(ctx.decrypt(c, np.uint32), a)
+    assert ctx.kernel_timing()[1] == 1
+    ctx.set_kernel_timing(False)
+    H.add_into(ctx, ca, cb, out)
+    assert ctx.kernel_timing() == (0.0, 0)
