@@ -471,8 +471,24 @@ __global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
         uint64_t *sw = st + (threadIdx.x & ~63u) * C;
         const uint64_t g0 = g - lane, lim = g0 < total ? (total - g0) * C : 0;
         const uint64_t *src = D.in.limbs + g0 * C;
-        for (uint32_t j = lane; j < 64 * C; j += 64)
-            if (j < lim) sw[j] = src[j];
+#ifndef HM_DECB_REGS
+#define HM_DECB_REGS 1 // (A/B knob) 0: a load -> LDS store loop (one load in flight per lane)
+#endif
+        if (HM_DECB_REGS) {
+            // all C (<= 8) loads of the lane in flight together, then the LDS stores
+            uint64_t v[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t j = lane + 64u * u;
+                v[u] = (u < C && j < lim) ? src[j] : 0ull;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u)
+                if (u < C) sw[lane + 64u * u] = v[u];
+        } else {
+            for (uint32_t j = lane; j < 64 * C; j += 64)
+                if (j < lim) sw[j] = src[j];
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
