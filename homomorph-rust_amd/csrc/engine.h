@@ -248,6 +248,10 @@ constexpr bool kMfWideLean = HM_MF_WIDE_LEAN;
 #define HM_MF_LEAN_LEAF_WORDS 224
 #endif
 constexpr uint32_t kMfLeanLeafWords = HM_MF_LEAN_LEAF_WORDS;
+#ifndef HM_MF_LEAN_LEAF_MIN
+#define HM_MF_LEAN_LEAF_MIN 193 // leaves narrower than this stay on the 3-wave instance (K = 16: 3,336-3,354 -> 3,389-3,406/s; configs[4]'s 224-word leaves unchanged)
+#endif
+constexpr uint32_t kMfLeanLeafMin = HM_MF_LEAN_LEAF_MIN;
 struct MulMfmaArgs {
     MulBase B;
     const void *tasks;

@@ -662,7 +662,7 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         // the lean instance for leaves up to kMfLeanLeafWords, when 16 waves' slices (4 blocks of 4)
         // fit a CU's 160 KB of LDS
         const uint32_t lw = mul_mfma_lean_leaf_wave_words(a.vmax, a.span, a.umax);
-        if (a.umax <= kMfLeanLeafWords && (256 + 4 * (size_t)lw) * 4 * 4 <= 160 * 1024)
+        if (a.umax <= kMfLeanLeafWords && a.umax >= kMfLeanLeafMin && (256 + 4 * (size_t)lw) * 4 * 4 <= 160 * 1024)
             a.lean = 1, a.wave_words = lw;
         if (launch_mul_mfma(a, true, st)) return hip_fail(c, hipGetLastError());
     } else {
