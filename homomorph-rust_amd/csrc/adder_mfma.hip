@@ -67,8 +67,9 @@ __device__ unsigned long long *g_mfma_prof; // 4 per wave, set by the harness
 #define HM_MFMA_PREFETCH 3
 #endif
 // the 25-chunk chain reads 4 ahead: configs[4] 925-929 -> 922-923 ms per 2^20 (2: 932-936,
-// 5: 926-927), measured when it ran at 2 waves per SIMD; at its current 3 waves per SIMD (168
-// VGPRs, HM_MFMA25_WPE) 3 vs 4 ahead was re-measured in round 5
+// 5: 926-927), measured when it ran at 2 waves per SIMD; re-measured in round 5 at its current
+// 3 waves per SIMD (168 VGPRs, HM_MFMA25_WPE): 3 ahead 881.1-883.7 ms, 4 ahead 881.4-884.4,
+// 5 ahead 898.4-898.5 (alternating on one box)
 #ifndef HM_MFMA_PREFETCH25
 #define HM_MFMA_PREFETCH25 4
 #endif
