@@ -224,6 +224,31 @@ __device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__rest
     uint32_t hiprev = 0u;
     // pv[k] is read one step ahead (the LDS latency hides under the step before), and each
     // residue class XORs its four products as one expression (v_bitop3 three-input XORs)
+#ifndef HM_CLMUL_PEEL
+#define HM_CLMUL_PEEL 1 // (A/B knob) last step peeled, clamped read-ahead, unconditional ds_xor
+#endif
+    if (HM_CLMUL_PEEL) {
+        if (nv <= 0) return;
+        uint32_t vnext = pv[0];
+        for (int k = 0; k < nv; ++k) {
+            const Holey V(vnext);
+            vnext = pv[min(k + 1, nv - 1)];
+            uint32_t zl[4], zh[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                uint64_t p[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) p[a] = (uint64_t)U.h[a] * V.h[(c - a) & 3];
+                zl[c] = xor4((uint32_t)p[0], (uint32_t)p[1], (uint32_t)p[2], (uint32_t)p[3]);
+                zh[c] = xor4((uint32_t)(p[0] >> 32), (uint32_t)(p[1] >> 32), (uint32_t)(p[2] >> 32),
+                             (uint32_t)(p[3] >> 32));
+            }
+            atomicXor(&out[k], holey_fold(zl) ^ hiprev);
+            hiprev = holey_fold(zh);
+        }
+        if (hiprev) atomicXor(&out[nv], hiprev);
+        return;
+    }
     uint32_t vnext = nv > 0 ? pv[0] : 0u;
     for (int k = 0; k <= nv; ++k) {
         uint32_t lo = 0u, hi = 0u;
