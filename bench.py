@@ -659,7 +659,11 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     H.mul_into(mctx, ca, cbb, co)  # sizes the workspace outside the timed loop
     mctx.synchronize()
     mreps = max(1, steps // 4)
-    wall, ev_s = time_loop(lambda: H.mul_into(mctx, ca, cbb, co), mreps, 1, 1, mctx.stream)
+    # the timed region as one replay of an mreps-step HIP graph, like the other legs (the
+    # multiply's ~dozens of launches per batch without host launch gaps; scripts/probe/mul_graph.py:
+    # bit-identical to direct launches)
+    wall, step_s, _, _ = timed_graph(mctx, lambda: H.mul_into(mctx, ca, cbb, co), mreps, 1, 1)
+    ev_s = step_s * mreps
     got = mctx.decrypt(co, np.uint8)
     # the oracle (1 thread) on the same workload: benches/u8.rs:9, 21-29 multiply u8 values at
     # (128, 128, 1, 128); two values per call, the engine context's keys, seeded masks
