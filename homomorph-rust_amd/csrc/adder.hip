@@ -31,22 +31,33 @@ __device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
 // Stage bits [i0, i0+nb) of one value's input (u64 limbs, exact degrees) into LDS words: bit
 // i0+t at dst + t*cnt, its word count at nw[t] (0 = null).  Lanes stride over the range's
 // contiguous limbs (all its bits at once, coalesced); every limb is validated against its bit's
-// degree word as in load_bit.  src/deg point at the value's first limb / degree word.
+// degree word as in load_bit.  src/deg point at the value's first limb / degree word.  tb: 2 nb
+// LDS words for the range's bounds and limb end offsets -- the per-lane bit cursor reads them
+// there, never from the by-value Bounds (dev_common.h: by-value argument arrays).
 __device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
                            const Bounds &B, uint32_t i0, uint32_t nb, uint32_t *dst, uint32_t cnt,
-                           uint32_t *nw, int *status) {
+                           uint32_t *nw, uint32_t *tb, int *status) {
     const int lane = lane_id();
+    i0 = rfl(i0), nb = rfl(nb);
     src += limb_off(B, i0);
     deg += i0;
-    uint32_t total = 0;
-    for (uint32_t t = 0; t < nb; ++t) total += cap_of(B.b[i0 + t]);
-    uint32_t t = 0, lo = 0, hi = nb ? cap_of(B.b[i0]) : 0;
+    uint32_t *bnd = tb, *ends = tb + nb;
+    // uniform pass: bounds and inclusive limb end offsets of the range's bits, scalar reads only
+    uint32_t total = 0, vb = 0, ve = 0;
+    for (uint32_t t = 0; t < nb; ++t) {
+        const uint32_t b = B.b[i0 + t];
+        total += cap_of(b);
+        if ((uint32_t)lane == t) vb = b, ve = total;
+    }
+    if ((uint32_t)lane < nb) bnd[lane] = vb, ends[lane] = ve;
+    wsync();
+    uint32_t t = 0, lo = 0, hi = nb ? ends[0] : 0;
     bool bad = false;
     for (uint32_t g = lane; g < total; g += kWave) {
-        while (g >= hi) ++t, lo = hi, hi += cap_of(B.b[i0 + t]);
+        while (g >= hi) ++t, lo = hi, hi = ends[t];
         const uint32_t d = deg[t], k = g - lo;
         uint64_t v = src[g];
-        if (d > B.b[i0 + t]) {
+        if (d > bnd[t]) {
             bad = true;
             continue;
         }
@@ -56,11 +67,11 @@ __device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, con
             continue;
         }
         if (k == nl - 1) {
-            const uint32_t tb = d % 64;
-            const uint64_t keep = (~0ull) >> (63 - tb);
+            const uint32_t top = d % 64;
+            const uint64_t keep = (~0ull) >> (63 - top);
             bad |= (v & ~keep) != 0;
             v &= keep;
-            if (d > 0 && !((v >> tb) & 1ull)) bad = true;
+            if (d > 0 && !((v >> top) & 1ull)) bad = true;
         }
         dst[t * cnt + 2 * k] = (uint32_t)v;
         dst[t * cnt + 2 * k + 1] = (uint32_t)(v >> 32);
@@ -70,7 +81,7 @@ __device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, con
     for (uint32_t k = lane; k < nb; k += kWave) {
         const uint32_t d = deg[k];
         uint32_t n = d / 32 + 1;
-        if (d > B.b[i0 + k] || (d == 0 && !(dst[k * cnt] & 1u))) n = 0;
+        if (d > bnd[k] || (d == 0 && !(dst[k * cnt] & 1u))) n = 0;
         nw[k] = n;
     }
 }
@@ -87,10 +98,12 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits [i0, i0 + nmine)
     const uint32_t i0 = min(L, part * bpw), nmine = min(L, i0 + bpw) - i0;
     // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][P: bpw cntP][na nb dAB dP]
+    //      [stage_bits' bound / end-offset table: 2 bpw]
     uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
     uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
     uint32_t *ABl = Xl + bpw * A.cntX, *Pl = ABl + bpw * A.cntAB;
     uint32_t *nAl = Pl + bpw * A.cntP, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
+    uint32_t *Tb = dP + bpw;
     uint32_t *ws = A.ws + e * A.ws_stride;
     uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
     uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
@@ -98,8 +111,8 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
 
     // stage + validate this wave's bits (every bit is validated, the last one too)
-    stage_bits(pa, da, A.ab, i0, nmine, Al, A.cntA, nAl, A.status);
-    stage_bits(pb, db, A.bb, i0, nmine, Bl, A.cntB, nBl, A.status);
+    stage_bits(pa, da, A.ab, i0, nmine, Al, A.cntA, nAl, Tb, A.status);
+    stage_bits(pb, db, A.bb, i0, nmine, Bl, A.cntB, nBl, Tb, A.status);
     for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
     // products only for bits < L-1 (the last bit has no outgoing carry)

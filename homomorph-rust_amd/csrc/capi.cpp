@@ -658,6 +658,9 @@ hm_status hm_encrypt_batch(hm_ctx *c, const uint8_t *data, uint32_t nbytes, cons
     for (uint32_t i = 0; i < out->nbits; ++i)
         if (out->bound[i] < c->pk_maxdeg) return HM_ERR_INVALID_ARGUMENT;
     if (out->n == 0) return HM_OK;
+    // launch_encrypt instantiates pk_cap <= 17 limbs; reject the rest BEFORE a mask draw (the
+    // encryption kernel advances the CSPRNG nonce: a draw without it would repeat its keystream)
+    if (c->pk_cap == 0 || c->pk_cap > 17) return HM_ERR_UNSUPPORTED;
     DeviceGuard g(c->device);
     EncArgs E{};
     E.pk = c->d_pk, E.tau = c->pk_tau, E.pk_cap = c->pk_cap;
@@ -781,7 +784,9 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         A.wpv = (uint32_t)std::max<uint64_t>(
             1, std::min<uint64_t>({std::max(want, rows_fit), 8, (uint64_t)L}));
         const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
-        A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 4 * bpw);
+        // (+ 2 bpw: stage_bits' per-lane bound / offset table; a wave's range is at most 64 bits)
+        if (bpw > 64) return HM_ERR_UNSUPPORTED;
+        A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 6 * bpw);
         if ((size_t)A.prep_lds * 4 * 4 > 160 * 1024) return HM_ERR_UNSUPPORTED;
     }
     // chain: a carry buffer holds a whole tile of the widest width instantiated (PAD mode);
@@ -982,6 +987,9 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
             const int rc = launch_poly_rem(poly_args(c, a, nullptr, out), T, c->stream);
             return rc ? hip_fail(c, hipGetLastError()) : HM_OK;
         }
+        // the cache is invalid from here until the new table is complete (a failed rebuild must
+        // not leave the old key matching a half-overwritten d_s)
+        c->rem_key.clear();
         std::vector<uint64_t> zt(ds * tcols, 0);
         // X^k mod S for the 64 k of column limb l0 + t: unit bits below deg S, then r = X * r mod
         // S; each block of 64 vectors is transposed word by word into the rows
@@ -1022,6 +1030,9 @@ hm_status hm_poly_rem_batch(hm_ctx *c, const hm_polys *a, const uint64_t *s, siz
         size_t have = c->d_s_limbs * 8;
         HM_HIP(c, grow(c, c->d_s, have, zt.size() * 8));
         c->d_s_limbs = have / 8;
+        // d_s is rewritten in place for another divisor: a graph captured with the old table
+        // (the cached path has no sync, so it is capturable) must refuse to replay
+        ++c->generation;
         HM_HIP(c, hipMemcpyAsync(c->d_s, zt.data(), zt.size() * 8, hipMemcpyHostToDevice, c->stream));
         HM_HIP(c, hipStreamSynchronize(c->stream)); // host buffer is released after return
         T = RemTable{c->d_s, (uint32_t)ds, (uint32_t)l0, (uint32_t)tcols};

@@ -130,8 +130,11 @@ __device__ __forceinline__ void enc_lookup2(uint32_t *acc, const uint4 *tab4, ui
 // The wave's 64 ciphertext bits t0 .. t0 + 63 once their subset sums are in acc: the plaintext
 // bit, the degree, and the stores (uniform caps: the wave's 64 * PC consecutive output limbs,
 // transposed through its LDS stage and stored coalesced; otherwise per bit at its offset)
+// sob / sooff: LDS copies of E.ob / E.ooff (the lane's bit k indexes them; a by-value argument
+// array is never indexed per lane, dev_common.h)
 template <int PC>
 __device__ __forceinline__ void enc_finish(const EncArgs &E, uint64_t *acc, uint64_t *st,
+                                           const uint32_t *sob, const uint32_t *sooff,
                                            uint64_t t0, uint64_t total, bool live, uint64_t e,
                                            uint32_t k, uint32_t nbits) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -143,7 +146,7 @@ __device__ __forceinline__ void enc_finish(const EncArgs &E, uint64_t *acc, uint
     for (int l = 0; l < PC; ++l)
         if (acc[l]) deg = l * 64 + 63 - __builtin_clzll(acc[l]);
     if (live) {
-        if ((uint32_t)deg > E.ob.b[k]) flag(E.status, HM_ERR_CAPACITY);
+        if ((uint32_t)deg > sob[k]) flag(E.status, HM_ERR_CAPACITY);
         E.out.degree[e * nbits + k] = (uint32_t)deg;
     }
     if (E.uniform_cap) {
@@ -164,8 +167,8 @@ __device__ __forceinline__ void enc_finish(const EncArgs &E, uint64_t *acc, uint
         }
         wsync();
     } else if (live) {
-        const uint32_t cap = cap_of(E.ob.b[k]);
-        uint64_t *dst = E.out.limbs + e * E.out.stride + E.ooff.b[k];
+        const uint32_t cap = cap_of(sob[k]);
+        uint64_t *dst = E.out.limbs + e * E.out.stride + sooff[k];
 #pragma unroll
         for (int l = 0; l < PC; ++l) {
             if ((uint32_t)l < cap) dst[l] = acc[l];
@@ -186,6 +189,7 @@ constexpr int kEncTabPairs = ((TOP1 ? PC - 1 : PC) + 1) / 2; // limb pairs per g
 
 template <int PC, bool TOP1>
 __device__ __forceinline__ void enc_bits_t128(const EncArgs &E, const uint4 *tab4, uint64_t *st,
+                                              const uint32_t *sob, const uint32_t *sooff,
                                               uint64_t t0, uint64_t total, uint32_t nbits,
                                               const uint4 &mw) {
     constexpr int PL = TOP1 ? PC - 1 : PC;      // limbs looked up (TOP1: E.pk_tab1, without the top)
@@ -217,7 +221,7 @@ __device__ __forceinline__ void enc_bits_t128(const EncArgs &E, const uint4 *tab
     uint64_t acc[PC];
 #pragma unroll
     for (int l = 0; l < PC; ++l) acc[l] = (uint64_t)a32[2 * l] | ((uint64_t)a32[2 * l + 1] << 32);
-    enc_finish<PC>(E, acc, st, t0, total, live, e, k, nbits);
+    enc_finish<PC>(E, acc, st, sob, sooff, t0, total, live, e, k, nbits);
 }
 
 // Copies a nibble table (G groups of NP limb pairs) into the block's LDS
@@ -243,11 +247,17 @@ encrypt_table_kernel(EncArgs E) {
     constexpr int NP = kEncTabPairs<PC, TOP1>; // limb pairs (TOP1: the table without the top limb)
     extern __shared__ uint64_t tab[];          // [G][NP][16][2] (upload_pk)
     const uint32_t G = GC ? GC : (E.tau + 3) / 4;
-    enc_table_to_lds<NP>(TOP1 ? E.pk_tab1 : E.pk_tab, G, tab);
-    const uint4 *tab4 = (const uint4 *)tab;
     uint64_t *stage = tab + (size_t)G * NP * 32; // [waves][64][PC] store transpose
     uint64_t *st = stage + (size_t)(threadIdx.x & ~63u) * PC;
     const uint32_t nbits = E.nbytes * 8;
+    // [HM_MAX_BITS] bounds, [HM_MAX_BITS] limb offsets per bit (after the transposes)
+    uint32_t *sob = (uint32_t *)(stage + (size_t)kEncBlock * PC), *sooff = sob + HM_MAX_BITS;
+    if (threadIdx.x < 64) {
+        arg_to_lds(E.ob.b, nbits, sob);
+        arg_to_lds(E.ooff.b, nbits, sooff);
+    }
+    enc_table_to_lds<NP>(TOP1 ? E.pk_tab1 : E.pk_tab, G, tab); // (its __syncthreads orders sob too)
+    const uint4 *tab4 = (const uint4 *)tab;
     const uint32_t mb = (E.tau + 7) / 8;
     const uint64_t total = E.n * nbits;
     // the loop runs per wave (the store transpose is wave-cooperative): lanes past the end of
@@ -262,7 +272,7 @@ encrypt_table_kernel(EncArgs E) {
         for (uint64_t t0 = first; t0 < total; t0 += step) {
             const uint4 cur = mw;
             if (t0 + step < total) mw = m4[min(t0 + step + lane, total - 1)]; // next iteration's
-            enc_bits_t128<PC, TOP1>(E, tab4, st, t0, total, nbits, cur);
+            enc_bits_t128<PC, TOP1>(E, tab4, st, sob, sooff, t0, total, nbits, cur);
         }
     } else {
         for (uint64_t t0 = first; t0 < total; t0 += step) {
@@ -288,7 +298,7 @@ encrypt_table_kernel(EncArgs E) {
                 for (uint32_t j = 0; j < ng; ++j)
                     enc_lookup<NP>(acc, tab4, g0 + j, (bits >> (4 * j)) & 15u);
             }
-            enc_finish<PC>(E, acc, st, t0, total, live, e, k, nbits);
+            enc_finish<PC>(E, acc, st, sob, sooff, t0, total, live, e, k, nbits);
         }
     }
     kt_finish(E.kt);
@@ -345,7 +355,8 @@ static void launch_enc_pc(const EncArgs &E, void *stream) {
     const size_t tab = (size_t)((E.tau + 3) / 4) * ((PC + 1) / 2) * 16 * 16;
     const size_t tab1 = (size_t)((E.tau + 3) / 4) * (PC / 2) * 16 * 16; // (top1: without the top limb)
     const bool t1 = E.tau == 128 && ((uintptr_t)E.masks & 15u) == 0 && E.top1 && PC > 1;
-    const size_t lds = (t1 ? tab1 : tab) + (size_t)kEncBlock * PC * 8; // + the store transpose
+    // + the store transpose + the per-bit bounds and offsets
+    const size_t lds = (t1 ? tab1 : tab) + (size_t)kEncBlock * PC * 8 + 2 * HM_MAX_BITS * 4;
     if (E.pk_tab && tab <= kEncTableBytes && lds <= 160 * 1024) { // one CU's LDS at most
         // a few resident blocks per CU, each striding over bits (the table copy is amortised)
         const uint64_t want = (threads + kEncBlock - 1) / kEncBlock;
@@ -497,14 +508,24 @@ __global__ void __launch_bounds__(256) decrypt_bits_kernel(DecArgs D) {
             for (uint32_t l = 0; l < C; ++l) acc ^= sw[lane * C + l] & D.z[l];
             p = (uint32_t)__builtin_popcountll(acc) & 1u;
         }
-    } else if (g < total) {
-        const uint64_t e = g / D.nbits;
-        const uint32_t k = (uint32_t)(g % D.nbits);
-        const uint64_t *src = D.in.limbs + e * D.in.stride + D.ioff.b[k];
-        const uint32_t cap = cap_of(D.ib.b[k]); // <= zlimbs (the host sizes z for the widest bit)
-        uint64_t acc = 0;
-        for (uint32_t l = 0; l < cap; ++l) acc ^= src[l] & D.z[l];
-        p = (uint32_t)__builtin_popcountll(acc) & 1u;
+    } else {
+        // lane-varying bit k: its bound and limb offset from LDS copies of D.ib / D.ioff (a
+        // by-value argument array is never indexed per lane, dev_common.h)
+        __shared__ __attribute__((aligned(16))) uint32_t sb[2 * HM_MAX_BITS];
+        if (threadIdx.x < 64) {
+            arg_to_lds(D.ib.b, D.nbits, sb);
+            arg_to_lds(D.ioff.b, D.nbits, sb + HM_MAX_BITS);
+        }
+        __syncthreads();
+        if (g < total) {
+            const uint64_t e = g / D.nbits;
+            const uint32_t k = (uint32_t)(g % D.nbits);
+            const uint64_t *src = D.in.limbs + e * D.in.stride + sb[HM_MAX_BITS + k];
+            const uint32_t cap = cap_of(sb[k]); // <= zlimbs (the host sizes z for the widest bit)
+            uint64_t acc = 0;
+            for (uint32_t l = 0; l < cap; ++l) acc ^= src[l] & D.z[l];
+            p = (uint32_t)__builtin_popcountll(acc) & 1u;
+        }
     }
     const uint64_t bits = __ballot(p);
     const uint64_t g0 = g - (uint64_t)lane_id();

@@ -30,6 +30,35 @@ __device__ __forceinline__ void gsync() {
 
 __device__ __forceinline__ uint32_t cap_of(uint32_t bound) { return bound / 64 + 1; }
 
+// ---------------------------------------------------------------------------------------------
+// By-value argument arrays (Bounds) are indexed with WAVE-UNIFORM indices only.  A lane-varying
+// index into a kernel argument compiles to vector loads from the kernarg segment (an address off
+// the kernarg SGPR pair, `v_lshl_add_u64 v, v, 2, s[0:1]` + `global_load_dword`) instead of scalar
+// loads -- the construct behind round 5's non-deterministic decrypt misreads.
+// tools/kernarg_audit.py checks every kernel of the library for it (tests/test_kernarg_audit.py).
+// Per-lane lookups go through LDS copies made here: the array is read with scalar loads
+// (uniform indices) and written to LDS by one lane.
+
+// the first n (wave-uniform, <= HM_MAX_BITS) entries of a into lds[0:n) (lds: HM_MAX_BITS words,
+// 16-byte aligned; entries past n up to the next multiple of 16 are written too), by the calling
+// wave: 16 entries per s_load_dwordx16, stored by lane 0 as four ds_write_b128.  Order them before
+// other lanes' (wsync) or other waves' (__syncthreads) reads.
+__device__ __forceinline__ void arg_to_lds(const uint32_t (&a)[HM_MAX_BITS], uint32_t n, uint32_t *lds) {
+    static_assert(HM_MAX_BITS % 16 == 0, "whole 16-entry chunks");
+    n = rfl(n);
+    const bool l0 = (threadIdx.x & 63u) == 0;
+    for (uint32_t c = 0; c < n; c += 16) { // uniform; c + 16 <= HM_MAX_BITS
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = a[c + j];
+        if (l0) {
+            uint4 *d = (uint4 *)(lds + c);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+    }
+}
+
 // Load one ciphertext bit (u64 limbs, exact degree `deg`) into 32-bit words at dst.
 // The degree word is validated against the limbs (top bit set, nothing above it).
 // Returns the word count (0 for the null polynomial).

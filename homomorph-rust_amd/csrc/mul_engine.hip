@@ -380,13 +380,18 @@ int launch_mul_deg(const MulDegArgs &A, void *stream) {
 
 // output degree words (exact; null -> 0) and the capacity check
 __global__ void __launch_bounds__(256) mul_final_kernel(MulFinalArgs F) {
+    // the lane's output bit i indexes an LDS copy of F.ob (a by-value argument array is never
+    // indexed per lane, dev_common.h)
+    __shared__ __attribute__((aligned(16))) uint32_t sob[HM_MAX_BITS];
+    if (threadIdx.x < 64) arg_to_lds(F.ob.b, F.K, sob);
+    __syncthreads();
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t e = t / F.K;
     const uint32_t i = (uint32_t)(t % F.K);
     if (e >= F.B.nv) return;
     const uint32_t d1 = F.B.deg1[(uint64_t)F.res[i] * F.B.nv + e];
     const uint32_t d = d1 ? d1 - 1 : 0u;
-    if (d > F.ob.b[i]) flag(F.B.status, HM_ERR_CAPACITY);
+    if (d > sob[i]) flag(F.B.status, HM_ERR_CAPACITY);
     F.out.degree[(F.B.e0 + e) * F.out.dstride + i] = d;
 }
 

@@ -786,13 +786,18 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 HM_HIP(c, hipEventRecord(c->ev_fork, c->stream));
                 HM_HIP(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
             }
+            hm_status kst = HM_OK;
             for (const KaProg &pg : col.ka)
-                if (hm_status st = run_ka(c, *P, pg, B, two && pg.lane ? c->aux_stream : c->stream); st)
-                    return st;
+                if ((kst = run_ka(c, *P, pg, B, two && pg.lane ? c->aux_stream : c->stream))) break;
             if (two) {
-                HM_HIP(c, hipEventRecord(c->ev_join, c->aux_stream));
-                HM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                // joined on every path, a failed lane's too: no unjoined fork under capture, and
+                // no auxiliary-stream work left running behind a caller that syncs c->stream only
+                const hipError_t e1 = hipEventRecord(c->ev_join, c->aux_stream);
+                const hipError_t e2 = hipStreamWaitEvent(c->stream, c->ev_join, 0);
+                if (kst == HM_OK && e1 != hipSuccess) return hip_fail(c, e1);
+                if (kst == HM_OK && e2 != hipSuccess) return hip_fail(c, e2);
             }
+            if (kst) return kst;
         }
         MulFinalArgs F{};
         F.B = B, F.res = (const uint32_t *)(T + P->off_res), F.K = K, F.out = oa;

@@ -195,8 +195,10 @@ hm_status hm_ctx_set_add_pipeline(hm_ctx *ctx, int enable);
  * times kernel k from now on (HM_TIME_OFF stops; setting resets the record and synchronizes the
  * stream): every launch of it made -- or captured into a graph -- while timing is on takes its
  * own record slot (up to 128), in which the kernel's waves stamp the device wall clock at their
- * start and end.  A captured launch's slot is refilled by every replay of its graph (the last
- * replay's stamps remain), so a K-step graph replayed once yields K launches.
+ * start and end (a minimum over starts, a maximum over ends).  A captured launch keeps its slot
+ * across replays and nothing clears it in between: the stamps are valid for ONE replay of the
+ * graph (R replays make each slot span from the first replay's start to the last one's end).  So
+ * enable, capture a K-step graph, replay it once, read: K launches (as the bench times it).
  * hm_ctx_kernel_timing synchronizes the stream and returns the summed duration (earliest wave
  * start to latest wave end, per slot) of the launches recorded and their number.
  * HM_TIME_ADD_CHAIN = 1 (hm_add_batch's carry chain, the dominant kernel of the add),

@@ -205,13 +205,19 @@ def test_kernel_timing_counts_direct_and_graph_launches(H):
     torch.cuda.synchronize()
     assert n == 3 and 0 < ms < ev0.elapsed_time(ev1)
     ctx.set_kernel_timing(True, "add_chain")  # reset
-    # three launches captured into one graph: three record slots, refilled by every replay
+    # three launches captured into one graph: three record slots, valid for one replay
     g = ctx.graph(lambda: [H.add_into(ctx, ca, cb, out) for _ in range(3)], warmup=0)
-    for _ in range(2):
-        g.replay()
+    ev0.record(ctx.stream)
+    g.replay()
+    ev1.record(ctx.stream)
+    ms1, n = ctx.kernel_timing()
     torch.cuda.synchronize()
-    ms, n = ctx.kernel_timing()
-    assert n == 3 and ms > 0
+    assert n == 3 and 0 < ms1 <= ev0.elapsed_time(ev1)
+    # without a reset a second replay extends every slot (documented in the header): the stamps
+    # then span both replays
+    g.replay()
+    ms2, n = ctx.kernel_timing()
+    assert n == 3 and ms2 > ms1
     got = ctx.decrypt(out, np.uint32)
     assert np.array_equal(got, (a + (a ^ 0xFFFF)).astype(np.uint32))
     ctx.set_kernel_timing(True, "encrypt")

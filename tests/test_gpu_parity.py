@@ -114,6 +114,16 @@ def test_poly_rem_table_cache(H, oracle):
             ref, rdeg = oracle.poly_rem(A[i], S)
             assert rd[i] == rdeg
             assert np.array_equal(rl[i, : len(ref)], ref) and not rl[i, len(ref):].any()
+    # a graph captured on S1's cached table refuses to replay once S2 rewrote the table in place
+    # (the rewrite keeps the buffer, so the generation must advance)
+    A = H.Polys.from_host(_rand_polys(rng, 32, 9), ctx.device)
+    g = ctx.graph(lambda: ctx.poly_rem(A, S1))
+    g.replay()
+    ctx.synchronize()
+    ctx.poly_rem(A, S2)
+    ctx.synchronize()
+    with pytest.raises(H.EngineError):
+        g.replay()
 
 
 def test_poly_rem_errors(H):
