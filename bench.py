@@ -235,7 +235,7 @@ def timed_graph(ctx, fn, reps, warmup, world=1, kernel=None):
             fn()
 
     gk = ctx.graph(steps, warmup=0)
-    wall, ev_s = time_loop(gk.replay, 1, 0, world)
+    wall, ev_s = time_loop(gk.replay, 1, 0, world, ctx.stream)  # (replays on the engine stream)
     ks, kn = None, 0
     if kernel:
         kms, kn = ctx.kernel_timing()
@@ -740,7 +740,8 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
     for name, k, nk in (("u32_mul_low12", 12, MUL_BATCH),
                         (f"u32_mul_low{MUL_LOW_BENCH}", MUL_LOW_BENCH, MUL_BATCH),
                         (f"u32_mul_low{MUL_LOW_BENCH}_batch{n32}", MUL_LOW_BENCH, n32),
-                        ("u32_mul_low20", 20, 16)):
+                        ("u32_mul_low20", 20, MUL_BATCH),
+                        ("u32_mul_low20_batch16", 20, 16)):
         ob = H.mul_out_bounds(c32a.bound[:k], c32b.bound[:k])
         va, vb = H.value_slice(c32a, 0, nk), H.value_slice(c32b, 0, nk)
         cp = H.Ciphered.empty(nk, ob, device)
@@ -763,7 +764,8 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
         out[name] = {
             "value": rate, "unit": f"u32 muls/s (result bits 0..{k - 1})", "batch": nk,
             "config": "configs[3] (batch 1024)" if nk == MUL_BATCH else
-                      f"aside: configs[3]'s circuit at batch {nk} (not configs[3]'s batch)",
+                      f"aside: configs[3]'s circuit at batch {nk} (not configs[3]'s batch; a "
+                      "labelled aside)",
             "ms_per_batch": 1e3 * wall / reps, "kernel_ms_per_batch": 1e3 * ev_s / reps,
             "decrypt_correct": int(np.sum(lo == want)), "of": nk, "key_seed": mseed,
             "secret_key_s0": int(mctx.get_secret_key().limbs[0] & 1),
@@ -771,8 +773,8 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
             "word_pairs_per_s": cost["word_pairs"] * rate,
             "bit_exact": "tests/test_golden.py (oracle fixtures: K=16, 8 values; K=20, 4 "
                          "values), test_gpu_properties.py (residue check of all 1024 K=16 "
-                         "products; K=20 Karatsuba = schoolbook + residue check), "
-                         "test_gpu_parity.py",
+                         "products; K=20 at batch 1024 under an S(0)=0 key: all decrypt, 64 "
+                         "by residue; K=20 Karatsuba = schoolbook), test_gpu_parity.py",
             "roofline": mul_roofline(mctx, c32a.bound, c32b.bound, k, nk, ev_s / reps,
                                      f"u32 multiply, low {k} bits"),
             "cpu_baseline": cpu_mul_low(k)}

@@ -335,7 +335,6 @@ struct RandArgs {
 // host-side launchers (kernels.hip)
 // bump false: the nonce is left for the caller's next launch to advance (EncArgs::nonce_bump)
 int launch_random(const RandArgs &a, void *stream, bool bump = true);
-// ev0/ev1 (hipEvent_t, may be null): recorded on the stream around the carry-chain launch
 int launch_add(const AddArgs &a, void *stream);
 int launch_add_prep(const AddArgs &a, void *stream);
 // the same add over values [e0, e0 + n) of a batch: argument block with every pointer advanced

@@ -742,11 +742,14 @@ class EngineGraph:
         self._ctx, self._g, self._gen = ctx, graph, generation
 
     def replay(self):
+        """Replay on the context's stream, so the replay is ordered with the context's other
+        launches (before it and after it) like the calls it captured."""
         if self._ctx.generation() != self._gen:
             raise EngineError(_lib.ERR_INVALID_ARGUMENT,
                               "graph replay: the context replaced a buffer this graph uses "
                               "(capture it again)")
-        self._g.replay()
+        with _torch().cuda.stream(self._ctx.stream):
+            self._g.replay()
 
 
 def add_into(ctx: Context, a: Ciphered, b: Ciphered, out: Ciphered) -> None:

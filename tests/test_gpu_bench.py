@@ -56,7 +56,9 @@ def test_bench_every_line_has_roofline_and_cpu_baseline():
     assert sec["u32_mul_low16"]["cpu_baseline"]["extrapolated"] is True
     # configs[3] names batch 1024; the batch-16384 rate is a labelled aside
     assert sec["u32_mul_low12"]["batch"] == sec["u32_mul_low16"]["batch"] == 1024
+    assert sec["u32_mul_low20"]["batch"] == 1024  # result bits 16..19 at configs[3]'s batch
     assert sec["u32_mul_low16_batch16384"]["batch"] == 16384
+    assert sec["u32_mul_low20_batch16"]["batch"] == 16
     assert sec["u32_mul_low12"]["cpu_baseline"].get("extrapolated") is None
     m = sec["mixed_config4"]
     assert m["verified"]["correct_sums"] == m["verified"]["correct_products"] == m["global_batch"]

@@ -12,11 +12,13 @@ properties (the oracle alone would take minutes to hours on the whole batches).
   configs[3] u32 mul (low 12 bits), batch 1024        every value's low 12 product bits decrypt
                                                       (up to noise); all 1024 bit-exact vs oracle
   configs[3] u32 mul (low 16 bits), batch 1024        under an S(0) = 0 key every product decrypts
-                                                      to a*b mod 2^16; K = 20 on two values,
+                                                      to a*b mod 2^16, all 1024 by residue
+  configs[3] u32 mul (low 20 bits), batch 1024        under an S(0) = 0 key every product decrypts
+                                                      to a*b mod 2^20, 64 by residue; on two values
                                                       Karatsuba = schoolbook
   configs[4] mixed add + mul-low-8, d=dp=tau=256,     the whole 2^20 global batch on one GPU through
              2^20 values                              bench.py's chunk loop: every value decrypts,
-                                                      64 sampled values bit-exact vs the oracle
+                                                      2048 sampled values bit-exact vs the oracle
 Every full batch is also checked polynomial by polynomial by the residue checksum
 (oracle/residue_check.c, tests/helpers.check_residues): residues mod a random X^64 + g form a
 ring homomorphism, so each output's residue must equal the reference circuit on the inputs'.
@@ -229,6 +231,31 @@ def test_mul_low16_config3_full_batch(H, oracle):
     want = ((a.astype(np.uint64) * b) & 0xFFFF).astype(np.uint16)
     assert np.array_equal(dec, want), int(np.sum(dec != want))
     assert helpers.check_residues(H, "mul", cp, ca, cb, k=k, seed=38) == n
+
+
+def test_mul_low20_config3_full_batch(H):
+    """configs[3] (u32 mul, batch 1024) at K = 20, the deepest prefix the bench runs: under an
+    S(0) = 0 key all 1024 products decrypt to a*b mod 2^20 (result bits 16..19 included), and a
+    64-value sample passes the residue check polynomial by polynomial (5 MB of output per value;
+    the K = 20 golden fixture pins 4 values bit for bit, tests/test_golden.py)."""
+    import torch
+    params, n, k = (128, 128, 1, 128), 1024, 20
+    seed = _s0_zero_seed(params)
+    ctx = make_ctx(H, params, seed)
+    assert not int(ctx.get_secret_key().limbs[0]) & 1
+    a, b = plain(n, np.uint32, 136), plain(n, np.uint32, 137)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)
+    cp = ctx.mul_low(ca, cb, k)
+    raw = ctx.decrypt_bytes(H.pad_bits(cp, 24)).cpu().numpy().astype(np.uint64)
+    ctx.synchronize()
+    got = raw[:, 0] | (raw[:, 1] << np.uint64(8)) | (raw[:, 2] << np.uint64(16))
+    want = (a.astype(np.uint64) * b) & np.uint64((1 << k) - 1)
+    assert np.array_equal(got, want), int(np.sum(got != want))
+    ns = 64
+    sub = lambda c: H.value_slice(c, 0, ns)  # noqa: E731
+    assert helpers.check_residues(H, "mul", sub(cp), sub(ca), sub(cb), k=k, seed=138) == ns
+    del cp
+    torch.cuda.empty_cache()
 
 
 def test_mul_low20_karatsuba_vs_schoolbook(H):
