@@ -49,6 +49,74 @@ def clmul(a: int, b: int) -> int:
     return r
 
 
+def clmul_fast(a: int, b: int, leaf: int = 1 << 15) -> int:
+    """The same product for operands of millions of bits (the golden multiply prefixes): an 8-bit
+    window table over the shorter operand below `leaf` bits, Karatsuba above (z1 = (a0+a1)(b0+b1)
+    - z0 - z2, exact over GF(2)[X]).  Checked against clmul in tests/test_oracle_circuits.py."""
+    la, lb = a.bit_length(), b.bit_length()
+    if la > lb:
+        a, b, la, lb = b, a, lb, la
+    if la <= 64:
+        return clmul(a, b)
+    if la <= leaf:
+        t = [0] * 256
+        for i in range(1, 256):
+            low = i & -i
+            t[i] = t[i ^ low] ^ (b << (low.bit_length() - 1))
+        r, sh = 0, 0
+        while a:
+            r ^= t[a & 255] << sh
+            a >>= 8
+            sh += 8
+        return r
+    h = lb // 2
+    m = (1 << h) - 1
+    if la <= h:  # unbalanced: split the longer operand only
+        return clmul_fast(a, b & m, leaf) ^ (clmul_fast(a, b >> h, leaf) << h)
+    a0, a1, b0, b1 = a & m, a >> h, b & m, b >> h
+    z0, z2 = clmul_fast(a0, b0, leaf), clmul_fast(a1, b1, leaf)
+    z1 = clmul_fast(a0 ^ a1, b0 ^ b1, leaf) ^ z0 ^ z2
+    return z0 ^ (z1 << h) ^ (z2 << (2 * h))
+
+
+def residue_int(p: int, g: int) -> int:
+    """P mod f, f = X^64 + g (deg g < 64): P = P_hi X^h + P_lo folds to P_hi (X^h mod f) + P_lo,
+    halving P's length per fold (X^h mod f by square-and-multiply in the residue ring).  P -> P mod
+    f is a ring homomorphism, so a circuit's output residues equal the circuit run on its inputs'
+    residues (mul_circuit(..., mul=residue_mul(g))): the model's own form of
+    oracle/residue_check.c, for products far too big for the model's circuit itself."""
+    mul = residue_mul(g)
+
+    def xpow(e):  # X^e mod f
+        r, base = 1, 2
+        while e:
+            if e & 1:
+                r = mul(r, base)
+            base = mul(base, base)
+            e >>= 1
+        return r
+
+    while p.bit_length() > 128:
+        h = p.bit_length() // 2
+        p = clmul(p >> h, xpow(h)) ^ (p & ((1 << h) - 1))
+    return mul(p, 1) if p >> 64 else p
+
+
+def residue_limbs(limbs, g: int) -> int:
+    """residue_int of a polynomial given as little-endian u64 limbs"""
+    return residue_int(limbs_to_int(limbs), g)
+
+
+def residue_mul(g: int):
+    """The product of the residue ring GF(2)[X]/(X^64 + g) on reduced operands."""
+    def mul(a: int, b: int) -> int:
+        t = clmul(a, b)
+        while t >> 64:
+            t = (t & MASK64) ^ clmul(t >> 64, g)
+        return t
+    return mul
+
+
 def gf2_mod(a: int, s: int) -> int:
     if s == 0:
         raise ZeroDivisionError("attempt to divide by zero")
@@ -99,9 +167,12 @@ def add_circuit(a: list[int], b: list[int]) -> list[int]:
     return out
 
 
-def mul_circuit(a: list[int], b: list[int], signed: bool = False) -> list[int]:
+def mul_circuit(a: list[int], b: list[int], signed: bool = False, mul=clmul) -> list[int]:
+    """The carry-save array of common.rs:66-105 (:115-155 signed).  `mul`: the ring product
+    (clmul; clmul_fast for big operands; a product mod f for the residue ring)."""
+    clmul_ = mul
     L = len(a)
-    pp = [[clmul(a[j], b[k]) for k in range(L)] for j in range(L)]
+    pp = [[clmul_(a[j], b[k]) for k in range(L)] for j in range(L)]
     if signed:
         pp[0][L - 1] ^= 1
         pp[L - 1][0] ^= 1
@@ -112,21 +183,18 @@ def mul_circuit(a: list[int], b: list[int], signed: bool = False) -> list[int]:
         for j in range(i + 1):
             p = pp[j][i - j]
             if i + 1 < L:
-                nxt.append(clmul(p, res[i]))
+                nxt.append(clmul_(p, res[i]))
             res[i] ^= p
         for c in prev:
             if i + 1 < L:
-                nxt.append(clmul(res[i], c))
+                nxt.append(clmul_(res[i], c))
             res[i] ^= c
         prev = nxt
     return res
 
 
 def limbs_to_int(limbs) -> int:
-    v = 0
-    for k, w in enumerate(limbs):
-        v |= int(w) << (64 * k)
-    return v
+    return int.from_bytes(b"".join(int(w).to_bytes(8, "little") for w in limbs), "little")
 
 
 def int_to_limbs(v: int, cap: int) -> list[int]:

@@ -12,6 +12,7 @@ the batch layout of include/homomorph_gpu.h, the masks that made them, the opera
 and the oracle's decryption of it.
 
     python tests/golden/make_golden.py      # rewrites tests/golden/*.npz
+    python tests/golden/make_golden.py --model-check-saved mullow20_u32_d128   # see model_check_saved
 """
 from __future__ import annotations
 
@@ -26,8 +27,8 @@ for p in (ROOT, os.path.join(ROOT, "homomorph-rust_amd"), os.path.join(ROOT, "te
     if p not in sys.path:
         sys.path.insert(0, p)
 
-from helpers import (as_bytes, bit_ints, fresh_bound, low_bits, masks, pad_bits_host, plain,  # noqa: E402
-                     digest)
+from helpers import (as_bytes, bit_ints, fresh_bound, low_bits, masks, offsets, pad_bits_host,  # noqa: E402
+                     plain, digest)
 from oracle import gf2_model as model  # noqa: E402
 from oracle import oracle_py as oracle  # noqa: E402
 
@@ -82,6 +83,51 @@ def _check_model(op, la, da, lb, db, bound, lo, do, obound, n):
         assert [model.degree(x) for x in ref] == degs.tolist()
 
 
+MODEL_RESIDUE_SEED = 0x6D6F64656C  # the model's residue modulus f = X^64 + g, g from SplitMix64
+
+
+def model_check_mullow(z, lo=None, values=(0,)):
+    """Cross-check a low-k multiply fixture against the big-int model (oracle/gf2_model.py).
+
+    - k <= 16: the model's own carry-save circuit (mul_circuit over clmul_fast) on `values`, whose
+      output degrees and per-value SHA-256 must equal the fixture's;
+    - with the product limbs `lo` (at generation; K = 20 takes the model hours per value): every
+      value's output residues mod f = X^64 + g (the model's residue_int) against the circuit run on
+      the inputs' residues (a ring homomorphism), and the product's digests against the fixture's.
+    Returns a description of what was checked (stored in the fixture as `model_check`)."""
+    k, bound, ob = int(z["k"]), z["in_bound"], z["out_bound"]
+    n = len(z["a_plain"])
+    la, da, b1 = low_bits(z["a_limbs"], z["a_degree"], bound, n, k)
+    lb, db, b2 = low_bits(z["b_limbs"], z["b_degree"], bound, n, k)
+    _, cap, _ = offsets(ob)
+    done = []
+    if k <= 16:
+        for e in values:
+            ref = model.mul_circuit(bit_ints(la, da, b1, e), bit_ints(lb, db, b2, e), mul=model.clmul_fast)
+            degs = np.asarray(z["out_degree"]).reshape(n, k)[e]
+            assert [model.degree(x) for x in ref] == degs.tolist(), f"model degrees, value {e}"
+            limbs = np.concatenate([np.array(model.int_to_limbs(x, int(c)), dtype=np.uint64)
+                                    for x, c in zip(ref, cap)])
+            assert digest(limbs, ob, 1)[0] == str(z["out_sha256"][e]), f"model SHA-256, value {e}"
+        done.append(f"model circuit (gf2_model.mul_circuit, clmul_fast) = fixture on values "
+                    f"{list(values)}")
+    if lo is not None:
+        assert digest(lo, ob, n) == [str(x) for x in z["out_sha256"]], "product != fixture"
+        g = model.splitmix64([MODEL_RESIDUE_SEED])
+        mul = model.residue_mul(g)
+        off, _, stride = offsets(ob)
+        lo2 = np.asarray(lo, dtype=np.uint64).reshape(n, stride)
+        for e in range(n):
+            ra = [model.residue_int(x, g) for x in bit_ints(la, da, b1, e)]
+            rb = [model.residue_int(x, g) for x in bit_ints(lb, db, b2, e)]
+            want = model.mul_circuit(ra, rb, mul=mul)
+            got = [model.residue_limbs(lo2[e, off[i]:off[i] + cap[i]], g) for i in range(k)]
+            assert got == want, f"model residues, value {e}"
+        done.append(f"model residues mod X^64 + g of all {n} values = the circuit on the inputs' "
+                    "residues (gf2_model.residue_int)")
+    return "; ".join(done)
+
+
 def make(name):
     import homomorph as H
     op, params, dtype, n, seed = CASES[name]
@@ -124,6 +170,7 @@ def make(name):
         out.update(k=np.array(k), out_bound=ob, out_degree=do,
                    out_sha256=np.array(digest(lo, ob, n)), out_plain=val,
                    expected_plain=(a.astype(np.uint64) * b.astype(np.uint64)) % (1 << k))
+        out["model_check"] = np.array(model_check_mullow(out, lo))
     elif op == "encdec":
         dec = oracle.decrypt_batch(sk, la, da, bound, nbits, n).view(dtype).reshape(-1)
         out.update(out_bound=bound, out_limbs=la, out_degree=da, out_plain=dec,
@@ -151,7 +198,24 @@ def make(name):
     print(f"{name}: {os.path.getsize(path)} B, decrypts correctly for {ok}/{n}")
 
 
+def model_check_saved(name):
+    """Model-check an existing low-k multiply fixture against the product its generation saved
+    (.NAME_product.npz, not committed: 20 MB at K = 20), without re-running the oracle, and record
+    the check in the fixture (`model_check`)."""
+    path = os.path.join(HERE, f"{name}.npz")
+    z = dict(np.load(path, allow_pickle=False))
+    prod = os.path.join(HERE, f".{name}_product.npz")
+    lo = np.load(prod, allow_pickle=False)["lo"] if os.path.exists(prod) else None
+    z["model_check"] = np.array(model_check_mullow(z, lo))
+    np.savez(path, **z)
+    print(name, str(z["model_check"]))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["--model-check-saved"]:
+        for name in sys.argv[2:]:
+            model_check_saved(name)
+        sys.exit(0)
     oracle.build()
     for name in (sys.argv[1:] or CASES):
         make(name)

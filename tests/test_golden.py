@@ -91,6 +91,22 @@ def _check_mullow_plain(g, dec, k, n):
     assert np.array_equal(val & 0xFF, g["expected_plain"] & 0xFF)
 
 
+@pytest.mark.parametrize("name", [f for f in FIXTURES if f.startswith("mullow")])
+def test_mullow_fixture_model_cross_check(name):
+    """The low-k multiply fixtures rest on the oracle AND the independent big-int model: at
+    generation every value's output residues were checked by the model (make_golden.py
+    model_check_mullow, recorded as `model_check`), and for k <= 16 the model's own carry-save
+    circuit reproduces value 0's degrees and SHA-256 here (~20 s)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+    g = load(name)
+    rec = str(g.get("model_check", ""))
+    assert "model residues" in rec and "all" in rec, rec
+    if int(g["k"]) <= 16:
+        assert "model circuit" in make_golden.model_check_mullow(g, values=(0,))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", FIXTURES)
 def test_gpu_reproduces_golden(name):
