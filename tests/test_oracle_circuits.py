@@ -156,3 +156,22 @@ def test_mul_low_bits_identity(oracle, signed):
     l8, d8 = oracle.mul_batch(la8, da8, b8, lb8, db8, b8, k, n, ob8)
     got_l, got_d, _ = low_bits(lo, do, ob, n, k)
     assert np.array_equal(got_d, d8) and np.array_equal(got_l, l8)
+
+
+def test_model_fast_product_and_residues():
+    """The model's big-operand tools used by the golden multiply prefixes (make_golden.py):
+    clmul_fast (window + Karatsuba) equals clmul, residue_int equals long division by X^64 + g,
+    and residue_mul is the product of the residue ring."""
+    rng = np.random.default_rng(71)
+    for la, lb in ((1, 1), (63, 200), (1000, 1000), (40000, 70000), (100000, 30)):
+        a = int.from_bytes(rng.bytes(la // 8 + 1), "little") >> (7 - la % 8)
+        b = int.from_bytes(rng.bytes(lb // 8 + 1), "little") >> (7 - lb % 8)
+        assert model.clmul_fast(a, b) == model.clmul(a, b), (la, lb)
+    g = int(rng.integers(0, 2**63)) | 1
+    f = (1 << 64) ^ g
+    for n in (5, 64, 65, 129, 3000):
+        p = int.from_bytes(rng.bytes(n // 8 + 1), "little")
+        assert model.residue_int(p, g) == model.gf2_mod(p, f), n
+    x, y = int.from_bytes(rng.bytes(300), "little"), int.from_bytes(rng.bytes(200), "little")
+    mul = model.residue_mul(g)
+    assert mul(model.gf2_mod(x, f), model.gf2_mod(y, f)) == model.gf2_mod(model.clmul(x, y), f)
