@@ -73,16 +73,20 @@ __device__ unsigned long long *g_mfma_prof; // 4 per wave, set by the harness
 #ifndef HM_MFMA_PREFETCH25
 #define HM_MFMA_PREFETCH25 4
 #endif
-template <int NC> constexpr int kPrefetchOf = NC > 16 ? HM_MFMA_PREFETCH25 : HM_MFMA_PREFETCH;
-// side(k) runs after MFMA k for k = 1, 4, 7 (the next tile's ring fill in three stages: its LDS
-// latency hides under this tile's MFMAs instead of stalling the wave between tiles)
+// (NC = 7, configs[0]'s d + d' = 128: 2 ahead, so that the ring fill's three stages fit before
+// the next tile's reads)
+template <int NC> constexpr int kPrefetchOf = NC > 16 ? HM_MFMA_PREFETCH25 : NC <= 8 ? 2 : HM_MFMA_PREFETCH;
+// side(k) runs after MFMA kStage<NC>(k) = 1, 4, 7 (NC = 7: 0, 2, 4): the next tile's ring fill in
+// three stages, its LDS latency hidden under this tile's MFMAs instead of stalling the wave between
+// tiles
+template <int NC> constexpr int kStage(int k) { return NC <= 8 ? 2 * k : 1 + 3 * k; }
 template <int NC, class Side, int kPrefetch = kPrefetchOf<NC>>
 __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[NC], const uint4 *rb, const uint4 *rbn,
                                           uint4 (&pf)[kPrefetch], v16f acc, Side &&side) {
     // pf holds this tile's first kPrefetch B fragments (read during the tile before); the last
     // kPrefetch reads of this tile fetch the next tile's (window base rbn; its ring fill is side
     // stage 2, issued above them), so the next tile's first MFMA does not wait for the LDS
-    static_assert(NC - kPrefetch > 7, "next tile's B reads must follow its ring fill (stage 2, after MFMA 7)");
+    static_assert(NC - kPrefetch > kStage<NC>(2), "next tile's B reads must follow its ring fill (stage 2)");
     uint4 bq[NC];
 #pragma unroll
     for (int c = 0; c < kPrefetch; ++c) bq[c] = pf[c];
@@ -93,9 +97,9 @@ __device__ __forceinline__ v16f tile_mfma(const v8i (&Af)[NC], const uint4 *rb, 
         const v8i Bf = {(int)bq[c].x, (int)bq[c].y, (int)bq[c].z, (int)bq[c].w, 0, 0, 0, 0};
         acc = mfma_fp4(Af[c], Bf, acc);
         asm volatile("" : "+v"(acc)::"memory");
-        if (c == 1) side(0);
-        if (c == 4) side(1);
-        if (c == 7) side(2);
+        if (c == kStage<NC>(0)) side(0);
+        if (c == kStage<NC>(1)) side(1);
+        if (c == kStage<NC>(2)) side(2);
     }
     return acc;
 }
@@ -139,7 +143,8 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
 constexpr int kMfmaWpb = HM_MFMA_WPB;
 static_assert(kMfmaWpb <= kAddWavesPerBlock, "host LDS plan");
 
-// NC = 13: 4 waves per SIMD (configs[1]'s 4096 waves fill the chip at that), 128 VGPRs;
+// NC = 7: 4 waves per SIMD (HM_MFMA7_WPE: 108 VGPRs, no spills; 5 or 6 spill 18 / 28); NC = 13: 4 waves per SIMD (configs[1]'s 4096 waves
+// fill the chip at that), 128 VGPRs;
 // NC = 25: 3 waves per SIMD, 168 VGPRs (the 25 A fragments alone are 100; engine.h HM_MFMA25_WPE)
 template <int NC>
 __global__ void __launch_bounds__(64 * kMfmaWpb)
@@ -426,7 +431,8 @@ int launch_add_chain_mfma(const AddArgs &a, void *stream) {
 #define HM_LAUNCH_CHAIN(NCV)                                                                      \
     hipLaunchKernelGGL((add_chain_mfma_kernel<NCV>), dim3((unsigned)blocks), dim3(64 * wpb), lds,  \
                        (hipStream_t)stream, a)
-    if (a.mfma == MfmaCfg<13>::kChunks) HM_LAUNCH_CHAIN(13);
+    if (a.mfma == MfmaCfg<7>::kChunks) HM_LAUNCH_CHAIN(7);
+    else if (a.mfma == MfmaCfg<13>::kChunks) HM_LAUNCH_CHAIN(13);
     else if (a.mfma == MfmaCfg<25>::kChunks) HM_LAUNCH_CHAIN(25);
     else return -1;
 #undef HM_LAUNCH_CHAIN

@@ -828,7 +828,8 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
             return fits ? lds : 0u;
         };
         uint32_t nc = 0, lds = 0;
-        if ((lds = plan(MfmaCfg<13>{}))) nc = 13;
+        if ((lds = plan(MfmaCfg<7>{}))) nc = 7;
+        else if ((lds = plan(MfmaCfg<13>{}))) nc = 13;
         else if ((lds = plan(MfmaCfg<25>{}))) nc = 25;
         if (!c->fp4_mfma) nc = 0;
         A.mfma = c->add_chain != HM_ADD_CHAIN_VALU ? nc : 0u;

@@ -374,7 +374,8 @@ constexpr uint64_t kAddPipeMin = 1024; // values per half of a pipelined add (hm
 constexpr uint32_t kTimedLaunches = 128;  // launches hm_ctx_set_kernel_timing can record
 constexpr uint32_t kTimerWaves = 32768;   // stamp pairs per launch (waves beyond share them)
 // MFMA carry chain (adder_mfma.hip), one configuration per chunk count NC: P_i within 2 NC - 1
-// words (NC = 13: 25 words, d + d' <= 256; NC = 25: 49 words, d + d' <= 512), nibble ring slots
+// words (NC = 7: 13 words, d + d' <= 128, configs[0]; NC = 13: 25 words, d + d' <= 256; NC = 25:
+// 49 words, d + d' <= 512), nibble ring slots
 // (a power of two above a tile's 32 + 2 NC word window plus the 32 words filled ahead), zero carry
 // words below C (the deepest window reach), a bit's workspace record in one or two 64-word
 // LDS-DMAs, and the SIMD occupancy the A fragments (4 NC VGPRs) leave.
@@ -390,7 +391,12 @@ template <int NC> struct MfmaCfg {
 #ifndef HM_MFMA25_WPE
 #define HM_MFMA25_WPE 3
 #endif
-    static constexpr int kWavesPerEU = NC <= 16 ? 4 : HM_MFMA25_WPE;
+// NC = 7: its 7 A fragments leave room for more waves per SIMD (a u8 add at d + d' = 128 is a
+// short chain: more waves hide its per-bit phases)
+#ifndef HM_MFMA7_WPE
+#define HM_MFMA7_WPE 4
+#endif
+    static constexpr int kWavesPerEU = NC <= 8 ? HM_MFMA7_WPE : NC <= 16 ? 4 : HM_MFMA25_WPE;
     static constexpr int kStageWords = 2 * kRecWords * kAddWavesPerBlock; // static LDS per block
     // ring slots mirrored past the end (slot s < kMirror also at kMfmaRingSlots + s), so every
     // lane's window of 2 NC - 1 slots is contiguous wherever it starts
