@@ -50,6 +50,8 @@ __device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, con
         if ((uint32_t)lane == t) vb = b, ve = total;
     }
     if ((uint32_t)lane < nb) bnd[lane] = vb, ends[lane] = ve;
+    // slot words past a bit's own capacity (bits of smaller bounds than the slot's) read as zero
+    for (uint32_t k = lane; k < nb * cnt; k += kWave) dst[k] = 0u;
     wsync();
     uint32_t t = 0, lo = 0, hi = nb ? ends[0] : 0;
     bool bad = false;
@@ -57,16 +59,14 @@ __device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, con
         while (g >= hi) ++t, lo = hi, hi = ends[t];
         const uint32_t d = deg[t], k = g - lo;
         uint64_t v = src[g];
+        const uint32_t nl = d / 64 + 1;
         if (d > bnd[t]) {
             bad = true;
-            continue;
-        }
-        const uint32_t nl = d / 64 + 1;
-        if (k >= nl) {
+            v = 0; // (every staged word is written: the fixed-length product rows read them all)
+        } else if (k >= nl) {
             bad |= v != 0; // limbs above the degree must be zero (layout invariant)
-            continue;
-        }
-        if (k == nl - 1) {
+            v = 0;
+        } else if (k == nl - 1) {
             const uint32_t top = d % 64;
             const uint64_t keep = (~0ull) >> (63 - top);
             bad |= (v & ~keep) != 0;
@@ -86,6 +86,10 @@ __device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, con
     }
 }
 
+// NB, NAB > 0: the plan's b_i and ab_i slots hold exactly NB and NAB words (d + d' = 128 / 256 /
+// 512: 6 / 10 / 18 and 9 / 17 / 33), and the product rows run at those fixed lengths
+// (clmul_row_xor_fixed: unrolled, zero-padded); 0: lengths from the degrees
+template <int NB, int NAB>
 __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
     const uint32_t wave = rfl(threadIdx.x >> 6);
@@ -145,8 +149,13 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     for (uint32_t k = lane; k < nprod * A.cntP; k += kWave) Pl[k] = 0u;
     wsync();
     for_rows([&](uint32_t t, uint32_t q) {
-        if ((int)q < (int)nAl[t])
-            clmul_row_xor(Al[t * A.cntA + q], Bl + t * A.cntB, (int)nBl[t], ABl + t * A.cntAB + q);
+        if ((int)q < (int)nAl[t]) {
+            if constexpr (NB > 0) {
+                if (nBl[t]) clmul_row_xor_fixed<NB>(Al[t * A.cntA + q], Bl + t * NB, ABl + t * NAB + q);
+            } else {
+                clmul_row_xor(Al[t * A.cntA + q], Bl + t * A.cntB, (int)nBl[t], ABl + t * A.cntAB + q);
+            }
+        }
     });
     wsync();
     for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
@@ -159,9 +168,14 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     // phase 2: P_i = x_i ^ x_i * ab_i
     for_rows([&](uint32_t t, uint32_t q) {
         const int nx = max((int)nAl[t], (int)nBl[t]);
-        if ((int)q < nx)
-            clmul_row_xor(Xl[t * A.cntX + q], ABl + t * A.cntAB, bitwords((int)dAB[t]),
-                          Pl + t * A.cntP + q);
+        if ((int)q < nx) {
+            if constexpr (NAB > 0) {
+                if (dAB[t]) clmul_row_xor_fixed<NAB>(Xl[t * A.cntX + q], ABl + t * NAB, Pl + t * A.cntP + q);
+            } else {
+                clmul_row_xor(Xl[t * A.cntX + q], ABl + t * A.cntAB, bitwords((int)dAB[t]),
+                              Pl + t * A.cntP + q);
+            }
+        }
     });
     wsync();
     for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) {
@@ -313,8 +327,18 @@ int launch_add_prep(const AddArgs &a, void *stream) {
     // wpv waves per value, 4 waves per block
     const uint64_t waves = a.n * a.wpv;
     const uint64_t blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL(add_prep_kernel, dim3((unsigned)blocks), dim3(256),
-                       (size_t)a.prep_lds * 4 * 4, (hipStream_t)stream, a);
+    const size_t lds = (size_t)a.prep_lds * 4 * 4;
+#ifndef HM_PREP_FIXED
+#define HM_PREP_FIXED 1 // (A/B knob) 0: product rows at the degrees' lengths only
+#endif
+    if (HM_PREP_FIXED && a.cntB == 10 && a.cntAB == 17)
+        hipLaunchKernelGGL((add_prep_kernel<10, 17>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+    else if (HM_PREP_FIXED && a.cntB == 6 && a.cntAB == 9)
+        hipLaunchKernelGGL((add_prep_kernel<6, 9>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+    else if (HM_PREP_FIXED && a.cntB == 18 && a.cntAB == 33)
+        hipLaunchKernelGGL((add_prep_kernel<18, 33>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL((add_prep_kernel<0, 0>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

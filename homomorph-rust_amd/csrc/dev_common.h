@@ -302,6 +302,36 @@ __device__ __forceinline__ void clmul_row_xor(uint32_t u, const uint32_t *__rest
     }
 }
 
+// The same row with a compile-time multiplicand length NV (its LDS slot is zero-padded to NV
+// words, so words past the degree multiply as zeros): fully unrolled, every multiplicand word read
+// before the first product (NV LDS reads in flight, no read-ahead bookkeeping), no loop control.
+template <int NV>
+__device__ __forceinline__ void clmul_row_xor_fixed(uint32_t u, const uint32_t *__restrict__ pv,
+                                                    uint32_t *out) {
+    const Holey U(u);
+    uint32_t v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = pv[k];
+    uint32_t hiprev = 0u;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const Holey V(v[k]);
+        uint32_t zl[4], zh[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint64_t p[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) p[a] = (uint64_t)U.h[a] * V.h[(c - a) & 3];
+            zl[c] = xor4((uint32_t)p[0], (uint32_t)p[1], (uint32_t)p[2], (uint32_t)p[3]);
+            zh[c] = xor4((uint32_t)(p[0] >> 32), (uint32_t)(p[1] >> 32), (uint32_t)(p[2] >> 32),
+                         (uint32_t)(p[3] >> 32));
+        }
+        atomicXor(&out[k], holey_fold(zl) ^ hiprev);
+        hiprev = holey_fold(zh);
+    }
+    if (hiprev) atomicXor(&out[NV], hiprev); // (zero whenever the product fits its slot)
+}
+
 // Kernel timer (engine.h KTimer): lane 0 of every wave stamps the device wall clock (100 MHz)
 // at the kernel's entry and at its exit.  Fire-and-forget atomics on per-wave addresses: no
 // barrier, no LDS, no contention (an earlier form counted blocks out on one global counter with
