@@ -329,7 +329,7 @@ int launch_add_prep(const AddArgs &a, void *stream) {
     const uint64_t blocks = (waves + 3) / 4;
     const size_t lds = (size_t)a.prep_lds * 4 * 4;
 #ifndef HM_PREP_FIXED
-#define HM_PREP_FIXED 1 // (A/B knob) 0: product rows at the degrees' lengths only
+#define HM_PREP_FIXED 0 // (A/B knob) 1: product rows at the slots' fixed lengths (measured neutral, r06)
 #endif
     if (HM_PREP_FIXED && a.cntB == 10 && a.cntAB == 17)
         hipLaunchKernelGGL((add_prep_kernel<10, 17>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);

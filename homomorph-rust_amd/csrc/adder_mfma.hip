@@ -136,6 +136,23 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
     }
 }
 
+// Wait for bit i's record DMA (stage_rec) but not for the `young` sum stores the previous bit's
+// tiles issued after it: gfx9 vector memory operations complete in order, loads and stores alike
+// (the compiler itself waits with vmcnt(N) on a load that younger stores follow), so vmcnt(N) with
+// N <= young guarantees the older DMA has landed.  young is a lower bound the tile loop counts
+// (one store instruction per tile on the uniform full-tile branch).
+#ifndef HM_REC_WAIT_YOUNG
+#define HM_REC_WAIT_YOUNG 1 // (A/B knob) 0: vmcnt(0), waiting for every store too
+#endif
+__device__ __forceinline__ void wait_record(int young) {
+    if (!HM_REC_WAIT_YOUNG || young <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (young >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (young >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (young >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (young >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+}
+
 // waves per block (<= kAddWavesPerBlock, which the host plan's LDS check assumes)
 #ifndef HM_MFMA_WPB
 #define HM_MFMA_WPB kAddWavesPerBlock
@@ -227,10 +244,12 @@ add_chain_mfma_kernel(AddArgs A) {
     int nc = 0;    // carry words (0 = null carry, common.rs:39)
     int degc = -1; // the carry's degree
     int tw = -1;   // > 0: the previous bit's tiles stored sum words [cntX, min(tw, cap words))
+    int young = 0; // store instructions issued after bit i's record DMA (a lower bound)
     uint32_t offo = 0;
     for (uint32_t i = 0; i < L; ++i) {
         HM_PT(tw0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // bit i's record has landed
+        wait_record(young); // bit i's record has landed
+        young = 0;
         const uint32_t *rec = &stage[wave][i & 1][0];
         // s_i = x_i ^ carry_i (common.rs:43-47)
         HM_PT(t0);
@@ -391,10 +410,13 @@ add_chain_mfma_kernel(AddArgs A) {
             gprev = tnow;
             const uint32_t word = sw[0] | sw[1];
             const uint32_t v = word ^ abw;
+            // (wave-uniform first: a tile wholly inside [wlo, capn) needs no per-lane test; it
+            // issues exactly one store instruction, counted for the next bit's record wait)
+            const bool full = T >= 1 && 32 * T + 32 <= capn;
+            young += full ? 1 : 0;
             if (h == 0) {
                 C[W] = v;
-                // (wave-uniform first: a tile wholly inside [wlo, capn) needs no per-lane test)
-                if (T >= 1 && 32 * T + 32 <= capn) {
+                if (full) {
                     asm volatile("" ::: "memory");
                     son[W] = v;
                 } else if (W >= wlo && W < capn) son[W] = v;
