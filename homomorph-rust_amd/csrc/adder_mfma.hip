@@ -142,7 +142,7 @@ __device__ __forceinline__ void ring_fill(const uint32_t *C, uint32_t *ring, con
 // N <= young guarantees the older DMA has landed.  young is a lower bound the tile loop counts
 // (one store instruction per tile on the uniform full-tile branch).
 #ifndef HM_REC_WAIT_YOUNG
-#define HM_REC_WAIT_YOUNG 1 // (A/B knob) 0: vmcnt(0), waiting for every store too
+#define HM_REC_WAIT_YOUNG 0 // (A/B knob, measured slower: r06 chain 463-472 us with vmcnt(0) against 472-476 us)
 #endif
 __device__ __forceinline__ void wait_record(int young) {
     if (!HM_REC_WAIT_YOUNG || young <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -286,6 +286,26 @@ struct MulPPGArgs {
     uint32_t umax, vmax, span;        // largest factor, other factor (words), output tiles
     uint32_t wave_words;
 };
+// The same partial products on the VALU by product rows (mul_engine.hip mul_ppv_kernel, the adder
+// prep's method): one wave per value stages the input slots 0 .. nin - 1 into its LDS, computes
+// every a_j * b_k of the plan (tasks, flattened from the groups) with lanes over (product, word of
+// a_j) rows -- 16 v_mad_u64_u32 per 32x32 product, rows meeting in LDS by ds_xor -- and writes
+// the products and their degrees.  For fresh operands of at most kPPVWords words (d + d' <= 256),
+// where a product is only 5 MFMA chunks and the MFMA form is latency-bound (r05: 0.15 busy).
+#ifndef HM_PPV_WORDS
+#define HM_PPV_WORDS 12
+#endif
+constexpr uint32_t kPPVWords = HM_PPV_WORDS;
+struct MulPPVArgs {
+    MulBase B;
+    const MulPPTask *tasks; // {u slot (a_j), v slot (b_k), out slot, 0}
+    uint32_t ntasks;
+    uint32_t nin;        // input slots staged (2 K: a_j, b_j)
+    uint32_t inw;        // LDS words per staged input slot (>= every input slot's capacity)
+    uint32_t qw;         // rows per product: the widest a_j (words)
+    uint32_t outw;       // LDS words per product (>= qw + the widest b_k + 1)
+    uint32_t wave_words; // LDS words per wave
+};
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
 struct KaComb {
     uint32_t z0, z1, z2; // child results, 2h words each (z1 may be kKaNone)
@@ -353,6 +373,7 @@ int launch_ka_sum(const KaSumArgs &a, void *stream);
 int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
 int launch_mul_ppg(const MulPPGArgs &a, void *stream);
+int launch_mul_ppv(const MulPPVArgs &a, void *stream);
 uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 uint32_t mul_mfma_lean_leaf_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);

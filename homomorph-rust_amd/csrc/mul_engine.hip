@@ -110,6 +110,61 @@ __global__ void __launch_bounds__(256) mul_pp_kernel(MulPPArgs P) {
     if (lane_id() == 0) P.B.deg1[(uint64_t)T.out * P.B.nv + e] = (uint32_t)(top + 1);
 }
 
+// Partial products by rows (engine.h MulPPVArgs): one wave per value.  LDS per wave:
+// [IN: nin x inw words][deg1 of the inputs: nin][OUT: ntasks x outw words].  Row (t, q) XORs word
+// q of a_j times b_k into OUT_t from word q up (clmul_row_xor: one 32x32 product per step as 16
+// v_mad_u64_u32 of holey operands, dev_common.h); the products are exact, so the words equal the
+// MFMA form's (mul_ppg_kernel) and the reference's (polynomial.rs:252-310).
+__global__ void __launch_bounds__(256) mul_ppv_kernel(MulPPVArgs P) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t wave = rfl(threadIdx.x >> 6);
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= P.B.nv) return; // whole wave exits together
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t *IN = lds + (size_t)wave * P.wave_words, *DIN = IN + P.nin * P.inw;
+    uint32_t *OUT = DIN + P.nin;
+    const uint32_t *arena = P.B.arena + e * P.B.astride;
+    // inputs: every slot's words up to inw (zero past its capacity; slots are zero above their
+    // degree), and their degrees
+    for (uint32_t f = lane; f < P.nin * P.inw; f += kWave) {
+        const uint32_t s = f / P.inw, w = f % P.inw;
+        const MulSlot sl = P.B.slots[s];
+        IN[f] = w < sl.words ? arena[sl.off + w] : 0u;
+    }
+    for (uint32_t s = lane; s < P.nin; s += kWave) DIN[s] = P.B.deg1[(uint64_t)s * P.B.nv + e];
+    for (uint32_t f = lane; f < P.ntasks * P.outw; f += kWave) OUT[f] = 0u;
+    wsync();
+    // rows: lanes over (task t, word q of its a_j)
+    for (uint32_t f = lane; f < P.ntasks * P.qw; f += kWave) {
+        const uint32_t t = f / P.qw, q = f % P.qw;
+        const MulPPTask T = P.tasks[t];
+        const int nu = bitwords((int)DIN[T.a]), nv = bitwords((int)DIN[T.b]);
+        if ((int)q < nu && nv)
+            clmul_row_xor(IN[T.a * P.inw + q], IN + T.b * P.inw, nv, OUT + t * P.outw + q);
+    }
+    wsync();
+    uint32_t *aw = P.B.arena + e * P.B.astride;
+    // lanes over (task, word): every output slot's words (outw >= its capacity), then the degrees
+    for (uint32_t f = lane; f < P.ntasks * P.outw; f += kWave) {
+        const uint32_t t = f / P.outw, w = f % P.outw;
+        const MulSlot so = P.B.slots[P.tasks[t].out];
+        if (w < so.words) aw[so.off + w] = OUT[f];
+    }
+    for (uint32_t t = lane; t < P.ntasks; t += kWave) {
+        const MulPPTask T = P.tasks[t];
+        const uint32_t du = DIN[T.a], dv = DIN[T.b];
+        P.B.deg1[(uint64_t)T.out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+    }
+}
+
+int launch_mul_ppv(const MulPPVArgs &P, void *stream) {
+    if (!P.B.nv || !P.ntasks) return 0;
+    const uint64_t blocks = (P.B.nv + 3) / 4;
+    hipLaunchKernelGGL(mul_ppv_kernel, dim3((unsigned)blocks), dim3(256), (size_t)P.wave_words * 4 * 4,
+                       (hipStream_t)stream, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_mul_pp(const MulPPArgs &P, void *stream) {
     const uint64_t waves = P.B.nv * P.ntasks;
     if (!waves) return 0;

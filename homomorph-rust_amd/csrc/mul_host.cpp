@@ -119,6 +119,12 @@ struct MulPlan {
     std::vector<MulPPItem> ppg_items;
     uint32_t ppg_umax = 0, ppg_vmax = 0, ppg_span = 0;
     size_t off_ppg_groups = 0, off_ppg_items = 0;
+    // ... or on the VALU by rows (mul_ppv_kernel) when every factor fits kPPVWords words: the same
+    // items flattened to tasks {a_j slot, b_k slot, out slot}
+    bool ppv = false;
+    std::vector<MulPPTask> ppv_tasks;
+    uint32_t ppv_inw = 0, ppv_outw = 0;
+    size_t off_ppv = 0;
     std::vector<KaSum> ka_sums;
     std::vector<MulVTask> ka_vtasks;
     std::vector<MulVTile> ka_vtiles;
@@ -274,6 +280,20 @@ bool build_plan(MulPlan &P) {
             if (g.count) P.ppg_groups.push_back(g);
         }
         P.ppg_span = std::min<uint32_t>(kMfSpan, std::max<uint32_t>(1, (omax + 31) / 32));
+#ifndef HM_PPV
+#define HM_PPV 1 // (A/B knob) 0: the partial products on the matrix cores (mul_ppg_kernel) always
+#endif
+        P.ppv = HM_PPV && std::max(P.ppg_umax, P.ppg_vmax) <= kPPVWords;
+        if (P.ppv) {
+            for (const MulPPGroup &g : P.ppg_groups)
+                for (uint32_t it = g.first; it < g.first + g.count; ++it)
+                    P.ppv_tasks.push_back({g.u, P.ppg_items[it].v, P.ppg_items[it].out, 0u});
+            for (uint32_t s = 0; s < 2 * K; ++s) P.ppv_inw = std::max(P.ppv_inw, P.slots[s].words);
+            P.ppv_outw = std::max(omax, P.ppg_umax + P.ppg_vmax + 1);
+            // a block's four waves within one CU's LDS, else the MFMA form
+            const size_t ww = 2 * K * (P.ppv_inw + 1) + P.ppv_tasks.size() * P.ppv_outw;
+            if (ww * 4 * 4 > 160 * 1024) P.ppv = false, P.ppv_tasks.clear();
+        }
     }
     std::vector<Item> prev;
     P.res_bound.assign(K, -1);
@@ -509,6 +529,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_ppm = o, o = align(o + P.ppm.size() * sizeof(MulProdTask));
     P.off_ppg_groups = o, o = align(o + P.ppg_groups.size() * sizeof(MulPPGroup));
     P.off_ppg_items = o, o = align(o + P.ppg_items.size() * sizeof(MulPPItem));
+    P.off_ppv = o, o = align(o + P.ppv_tasks.size() * sizeof(MulPPTask));
     P.off_ka_sums = o, o = align(o + P.ka_sums.size() * sizeof(KaSum));
     P.off_ka_vtasks = o, o = align(o + P.ka_vtasks.size() * sizeof(MulVTask));
     P.off_ka_vtiles = o, o = align(o + P.ka_vtiles.size() * sizeof(MulVTile));
@@ -528,6 +549,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_ppm, P.ppm.data(), P.ppm.size() * sizeof(MulProdTask));
     put(P.off_ppg_groups, P.ppg_groups.data(), P.ppg_groups.size() * sizeof(MulPPGroup));
     put(P.off_ppg_items, P.ppg_items.data(), P.ppg_items.size() * sizeof(MulPPItem));
+    put(P.off_ppv, P.ppv_tasks.data(), P.ppv_tasks.size() * sizeof(MulPPTask));
     put(P.off_ka_sums, P.ka_sums.data(), P.ka_sums.size() * sizeof(KaSum));
     put(P.off_ka_vtasks, P.ka_vtasks.data(), P.ka_vtasks.size() * sizeof(MulVTask));
     put(P.off_ka_vtiles, P.ka_vtiles.data(), P.ka_vtiles.size() * sizeof(MulVTile));
@@ -728,7 +750,15 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
         S.B = B, S.a = batch_arg(a), S.b = batch_arg(b), S.K = K;
         fill_bounds(S.ab, a), fill_bounds(S.bb, b);
         if (launch_mul_stage(S, c->stream)) return hip_fail(c, hipGetLastError());
-        if (P->ppg && !P->ppg_groups.empty()) {
+        if (P->ppg && P->ppv && !P->ppv_tasks.empty()) {
+            MulPPVArgs v{};
+            v.B = B;
+            v.tasks = (const MulPPTask *)(T + P->off_ppv);
+            v.ntasks = (uint32_t)P->ppv_tasks.size();
+            v.nin = 2 * K, v.inw = P->ppv_inw, v.qw = P->ppg_umax, v.outw = P->ppv_outw;
+            v.wave_words = v.nin * (v.inw + 1) + v.ntasks * v.outw;
+            if (launch_mul_ppv(v, c->stream)) return hip_fail(c, hipGetLastError());
+        } else if (P->ppg && !P->ppg_groups.empty()) {
             MulPPGArgs g{};
             g.B = B;
             g.groups = (const MulPPGroup *)(T + P->off_ppg_groups);
