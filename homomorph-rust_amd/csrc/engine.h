@@ -306,6 +306,25 @@ struct MulPPVArgs {
     uint32_t outw;       // LDS words per product (>= qw + the widest b_k + 1)
     uint32_t wave_words; // LDS words per wave
 };
+// Small schoolbook carry products on the VALU by rows (mul_engine.hip mul_rows_kernel): one wave
+// per value, a column's products whose operands fit kRowsU x kRowsV words (slot capacities; the
+// 17 x 17 and 17 x 33-word carries of the u8 multiply's columns at d + d' = 256, MFMA "tiny" class
+// before), each product's operands staged in the wave's LDS, rows (product, word of u) as in
+// mul_ppv_kernel.  LDS per task: uw + vw + ow + 2 words.
+#ifndef HM_ROWS_U
+#define HM_ROWS_U 20
+#endif
+#ifndef HM_ROWS_V
+#define HM_ROWS_V 36
+#endif
+constexpr uint32_t kRowsU = HM_ROWS_U, kRowsV = HM_ROWS_V;
+struct MulRowArgs {
+    MulBase B;
+    const MulProdTask *tasks; // {u slot (fewer words), v slot, out slot}
+    uint32_t ntasks;
+    uint32_t uw, vw, ow;      // LDS words per task's u, v and product (slot capacities)
+    uint32_t wave_words;
+};
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)
 struct KaComb {
     uint32_t z0, z1, z2; // child results, 2h words each (z1 may be kKaNone)
@@ -374,6 +393,7 @@ int launch_mul_vprod(const MulVProdArgs &a, uint32_t w, void *stream);
 int launch_mul_mfma(const MulMfmaArgs &a, bool leaf, void *stream);
 int launch_mul_ppg(const MulPPGArgs &a, void *stream);
 int launch_mul_ppv(const MulPPVArgs &a, void *stream);
+int launch_mul_rows(const MulRowArgs &a, void *stream);
 uint32_t mul_mfma_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 uint32_t mul_mfma_lean_leaf_wave_words(uint32_t vmax, uint32_t span, uint32_t umax);
 int launch_ka_comb(const KaCombArgs &a, void *stream);

@@ -165,6 +165,63 @@ int launch_mul_ppv(const MulPPVArgs &P, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// A column's small carry products by rows (engine.h MulRowArgs): one wave per value.  LDS per
+// wave: per task [u: uw][v: vw][out: ow][deg u, deg v]; the products exact (= mul_mfma_kernel's).
+__global__ void __launch_bounds__(256) mul_rows_kernel(MulRowArgs P) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t wave = rfl(threadIdx.x >> 6);
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (e >= P.B.nv) return; // whole wave exits together
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t tw = P.uw + P.vw + P.ow + 2; // LDS words per task
+    uint32_t *W = lds + (size_t)wave * P.wave_words;
+    uint32_t *aw = P.B.arena + e * P.B.astride;
+    // operands (zero past their slot capacity; slots are zero above their degree), degrees, and
+    // zeroed products: lanes over (task, word of the task's block)
+    for (uint32_t f = lane; f < P.ntasks * tw; f += kWave) {
+        const uint32_t t = f / tw, w = f % tw;
+        const MulProdTask T = P.tasks[t];
+        uint32_t v = 0u;
+        if (w < P.uw) {
+            const MulSlot s = P.B.slots[T.u];
+            v = w < s.words ? aw[s.off + w] : 0u;
+        } else if (w < P.uw + P.vw) {
+            const MulSlot s = P.B.slots[T.v];
+            v = w - P.uw < s.words ? aw[s.off + w - P.uw] : 0u;
+        } else if (w == tw - 2) {
+            v = P.B.deg1[(uint64_t)T.u * P.B.nv + e];
+        } else if (w == tw - 1) {
+            v = P.B.deg1[(uint64_t)T.v * P.B.nv + e];
+        }
+        W[f] = v;
+    }
+    wsync();
+    for (uint32_t f = lane; f < P.ntasks * P.uw; f += kWave) {
+        const uint32_t t = f / P.uw, q = f % P.uw;
+        const uint32_t *Tw = W + t * tw;
+        const int nu = bitwords((int)Tw[tw - 2]), nv = bitwords((int)Tw[tw - 1]);
+        if ((int)q < nu && nv) clmul_row_xor(Tw[q], Tw + P.uw, nv, (uint32_t *)Tw + P.uw + P.vw + q);
+    }
+    wsync();
+    for (uint32_t f = lane; f < P.ntasks * P.ow; f += kWave) {
+        const uint32_t t = f / P.ow, w = f % P.ow;
+        const MulSlot so = P.B.slots[P.tasks[t].out];
+        if (w < so.words) aw[so.off + w] = W[t * tw + P.uw + P.vw + w];
+    }
+    for (uint32_t t = lane; t < P.ntasks; t += kWave) {
+        const uint32_t du = W[t * tw + tw - 2], dv = W[t * tw + tw - 1];
+        P.B.deg1[(uint64_t)P.tasks[t].out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+    }
+}
+
+int launch_mul_rows(const MulRowArgs &P, void *stream) {
+    if (!P.B.nv || !P.ntasks) return 0;
+    const uint64_t blocks = (P.B.nv + 3) / 4;
+    hipLaunchKernelGGL(mul_rows_kernel, dim3((unsigned)blocks), dim3(256), (size_t)P.wave_words * 4 * 4,
+                       (hipStream_t)stream, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_mul_pp(const MulPPArgs &P, void *stream) {
     const uint64_t waves = P.B.nv * P.ntasks;
     if (!waves) return 0;

@@ -100,6 +100,8 @@ struct MulPlan {
         uint32_t prod;             // MulProdTask offset (in tasks)
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
         MfLaunch mfl[3];                  // MFMA schoolbook products: tiny, narrow, wide
+        uint32_t rows = 0, nrows = 0;     // ... small ones on the VALU by rows (row_tasks range)
+        uint32_t rows_uw = 0, rows_vw = 0, rows_ow = 0;
         std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
@@ -112,6 +114,8 @@ struct MulPlan {
     std::vector<MulTile> mspans; // MFMA spans {task, first output word} of the schoolbook products
     std::vector<MulSpanRec> mrecs; // ... resolved (parallel to mspans; built after the regions)
     std::vector<MulProdTask> ppm; // partial products a_j * b_k run on the matrix cores
+    std::vector<MulProdTask> row_tasks; // small carry products on the VALU (Col::rows)
+    size_t off_rows = 0;
     // ... or, when every one fits (kMfPPGWords), all of them in one launch before the columns,
     // grouped by a_j (mul_ppg_kernel)
     bool ppg = false;
@@ -438,9 +442,34 @@ bool build_plan(MulPlan &P) {
         std::vector<MulTile> byw[kNW];
         std::vector<uint32_t> mfk[3]; // MFMA schoolbook products by class
         uint32_t omax[3] = {0, 0, 0};
+#ifndef HM_ROWS
+#define HM_ROWS 1 // (A/B knob) 0: the small products stay in the MFMA tiny class
+#endif
+        col.rows = (uint32_t)P.row_tasks.size();
+        auto rows_ok = [&](uint32_t k) {
+            const uint32_t uw = P.slots[P.prod[k].u].words, vw = P.slots[P.prod[k].v].words;
+            return HM_ROWS && P.mfma && !is_ka[k - col.prod] && uw >= kMfMinWords && uw <= kRowsU &&
+                   vw <= kRowsV;
+        };
+        for (uint32_t k = col.prod; k < P.prod.size(); ++k)
+            if (rows_ok(k)) {
+                col.rows_uw = std::max(col.rows_uw, P.slots[P.prod[k].u].words);
+                col.rows_vw = std::max(col.rows_vw, P.slots[P.prod[k].v].words);
+                col.rows_ow = std::max(col.rows_ow, P.slots[P.prod[k].out].words);
+                ++col.nrows;
+            }
+        col.rows_ow = std::max(col.rows_ow, col.rows_uw + col.rows_vw + 1);
+        // the column's small products on the VALU when a block's four waves' LDS fits one CU
+        const bool use_rows =
+            col.nrows && (size_t)col.nrows * (col.rows_uw + col.rows_vw + col.rows_ow + 2) * 4 * 4 <= 160 * 1024;
+        if (!use_rows) col.nrows = 0;
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
             if (is_ka[k - col.prod]) continue;
             const uint32_t uw = P.slots[P.prod[k].u].words;
+            if (use_rows && rows_ok(k)) {
+                P.row_tasks.push_back(P.prod[k]);
+                continue;
+            }
             if (P.mfma && uw >= kMfMinWords) {
                 const int cl = uw <= kMfTinyWords ? 0 : uw <= kMfNarrowWords ? 1 : 2;
                 mfk[cl].push_back(k);
@@ -522,6 +551,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_pp = o, o = align(o + P.pp.size() * sizeof(MulPPTask));
     P.off_lists = o, o = align(o + P.lists.size() * 4);
     P.off_prod = o, o = align(o + P.prod.size() * sizeof(MulProdTask));
+    P.off_rows = o, o = align(o + P.row_tasks.size() * sizeof(MulProdTask));
     P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
     P.off_mspans = o, o = align(o + P.mspans.size() * sizeof(MulTile));
@@ -542,6 +572,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_pp, P.pp.data(), P.pp.size() * sizeof(MulPPTask));
     put(P.off_lists, P.lists.data(), P.lists.size() * 4);
     put(P.off_prod, P.prod.data(), P.prod.size() * sizeof(MulProdTask));
+    put(P.off_rows, P.row_tasks.data(), P.row_tasks.size() * sizeof(MulProdTask));
     put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
     put(P.off_mspans, P.mspans.data(), P.mspans.size() * sizeof(MulTile));
@@ -795,6 +826,13 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             sc.out = oa, sc.out_off = ooff[i], sc.out_cap = cap_of(out->bound[i]);
             sc.chunks = (std::max(col.maxwords, 2 * sc.out_cap) + 255) / 256;
             if (launch_mul_scan(sc, c->stream)) return hip_fail(c, hipGetLastError());
+            if (col.nrows) {
+                MulRowArgs ra{};
+                ra.B = B, ra.tasks = (const MulProdTask *)(T + P->off_rows) + col.rows;
+                ra.ntasks = col.nrows, ra.uw = col.rows_uw, ra.vw = col.rows_vw, ra.ow = col.rows_ow;
+                ra.wave_words = col.nrows * (ra.uw + ra.vw + ra.ow + 2);
+                if (launch_mul_rows(ra, c->stream)) return hip_fail(c, hipGetLastError());
+            }
             for (const MfLaunch &m : col.mfl)
                 if (hm_status st = mf_launch(m, P->off_prod, col.prod); st) return st;
             for (uint32_t q = 0; q < kNW; ++q) {
