@@ -320,7 +320,8 @@ struct MulPPVArgs {
 constexpr uint32_t kRowsU = HM_ROWS_U, kRowsV = HM_ROWS_V;
 struct MulRowArgs {
     MulBase B;
-    const MulProdTask *tasks; // {u slot (fewer words), v slot, out slot}
+    const MulSpanRec *recs; // resolved tasks: u / v / out offsets, out words, slots; base =
+                            // u words | v words << 16 (slot capacities)
     uint32_t ntasks;
     uint32_t uw, vw, ow;      // LDS words per task's u, v and product (slot capacities)
     uint32_t wave_words;

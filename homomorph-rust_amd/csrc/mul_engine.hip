@@ -175,42 +175,45 @@ __global__ void __launch_bounds__(256) mul_rows_kernel(MulRowArgs P) {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t tw = P.uw + P.vw + P.ow + 2; // LDS words per task
     uint32_t *W = lds + (size_t)wave * P.wave_words;
+    uint32_t *R = W + P.ntasks * tw; // per task: uoff voff ooff nout words oslot (6 words)
     uint32_t *aw = P.B.arena + e * P.B.astride;
-    // operands (zero past their slot capacity; slots are zero above their degree), degrees, and
-    // zeroed products: lanes over (task, word of the task's block)
+    // the host-resolved records (one load), then the operands' degrees (one dependent load)
+    for (uint32_t t = lane; t < P.ntasks; t += kWave) {
+        const MulSpanRec r = P.recs[t];
+        uint32_t *Rt = R + 6 * t;
+        Rt[0] = r.uoff, Rt[1] = r.voff, Rt[2] = r.ooff, Rt[3] = r.nout, Rt[4] = r.base, Rt[5] = r.oslot;
+        W[t * tw + tw - 2] = P.B.deg1[(uint64_t)r.uslot * P.B.nv + e];
+        W[t * tw + tw - 1] = P.B.deg1[(uint64_t)r.vslot * P.B.nv + e];
+    }
+    wsync();
+    // operands (zero past their slot capacity; slots are zero above their degree) and zeroed
+    // products: lanes over (task, word of the task's block)
     for (uint32_t f = lane; f < P.ntasks * tw; f += kWave) {
         const uint32_t t = f / tw, w = f % tw;
-        const MulProdTask T = P.tasks[t];
+        if (w >= tw - 2) continue;
+        const uint32_t *Rt = R + 6 * t;
+        const uint32_t uw = Rt[4] & 0xFFFFu, vw = Rt[4] >> 16;
         uint32_t v = 0u;
-        if (w < P.uw) {
-            const MulSlot s = P.B.slots[T.u];
-            v = w < s.words ? aw[s.off + w] : 0u;
-        } else if (w < P.uw + P.vw) {
-            const MulSlot s = P.B.slots[T.v];
-            v = w - P.uw < s.words ? aw[s.off + w - P.uw] : 0u;
-        } else if (w == tw - 2) {
-            v = P.B.deg1[(uint64_t)T.u * P.B.nv + e];
-        } else if (w == tw - 1) {
-            v = P.B.deg1[(uint64_t)T.v * P.B.nv + e];
-        }
+        if (w < P.uw) v = w < uw ? aw[Rt[0] + w] : 0u;
+        else if (w < P.uw + P.vw) v = w - P.uw < vw ? aw[Rt[1] + w - P.uw] : 0u;
         W[f] = v;
     }
     wsync();
     for (uint32_t f = lane; f < P.ntasks * P.uw; f += kWave) {
         const uint32_t t = f / P.uw, q = f % P.uw;
-        const uint32_t *Tw = W + t * tw;
+        uint32_t *Tw = W + t * tw;
         const int nu = bitwords((int)Tw[tw - 2]), nv = bitwords((int)Tw[tw - 1]);
-        if ((int)q < nu && nv) clmul_row_xor(Tw[q], Tw + P.uw, nv, (uint32_t *)Tw + P.uw + P.vw + q);
+        if ((int)q < nu && nv) clmul_row_xor(Tw[q], Tw + P.uw, nv, Tw + P.uw + P.vw + q);
     }
     wsync();
     for (uint32_t f = lane; f < P.ntasks * P.ow; f += kWave) {
         const uint32_t t = f / P.ow, w = f % P.ow;
-        const MulSlot so = P.B.slots[P.tasks[t].out];
-        if (w < so.words) aw[so.off + w] = W[t * tw + P.uw + P.vw + w];
+        const uint32_t *Rt = R + 6 * t;
+        if (w < Rt[3]) aw[Rt[2] + w] = W[t * tw + P.uw + P.vw + w];
     }
     for (uint32_t t = lane; t < P.ntasks; t += kWave) {
         const uint32_t du = W[t * tw + tw - 2], dv = W[t * tw + tw - 1];
-        P.B.deg1[(uint64_t)P.tasks[t].out * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
+        P.B.deg1[(uint64_t)R[6 * t + 5] * P.B.nv + e] = (du && dv) ? du + dv - 1 : 0u;
     }
 }
 

@@ -115,6 +115,7 @@ struct MulPlan {
     std::vector<MulSpanRec> mrecs; // ... resolved (parallel to mspans; built after the regions)
     std::vector<MulProdTask> ppm; // partial products a_j * b_k run on the matrix cores
     std::vector<MulProdTask> row_tasks; // small carry products on the VALU (Col::rows)
+    std::vector<MulSpanRec> row_recs;   // ... resolved (built after the regions)
     size_t off_rows = 0;
     // ... or, when every one fits (kMfPPGWords), all of them in one launch before the columns,
     // grouped by a_j (mul_ppg_kernel)
@@ -461,7 +462,7 @@ bool build_plan(MulPlan &P) {
         col.rows_ow = std::max(col.rows_ow, col.rows_uw + col.rows_vw + 1);
         // the column's small products on the VALU when a block's four waves' LDS fits one CU
         const bool use_rows =
-            col.nrows && (size_t)col.nrows * (col.rows_uw + col.rows_vw + col.rows_ow + 2) * 4 * 4 <= 160 * 1024;
+            col.nrows && (size_t)col.nrows * (col.rows_uw + col.rows_vw + col.rows_ow + 8) * 4 * 4 <= 160 * 1024;
         if (!use_rows) col.nrows = 0;
         for (uint32_t k = col.prod; k < P.prod.size(); ++k) {
             if (is_ka[k - col.prod]) continue;
@@ -541,6 +542,11 @@ bool build_plan(MulPlan &P) {
         resolve(col.ppl, P.ppm, col.ppm);
         for (const MfLaunch &m : col.mfl) resolve(m, P.prod, col.prod);
     }
+    // the row products resolved (base: the operands' slot capacities, u | v << 16)
+    for (const MulProdTask &t : P.row_tasks)
+        P.row_recs.push_back(MulSpanRec{P.slots[t.u].off, P.slots[t.v].off, P.slots[t.out].off,
+                                        P.slots[t.out].words, t.u, t.v, t.out,
+                                        P.slots[t.u].words | (P.slots[t.v].words << 16)});
     return true;
 }
 
@@ -551,7 +557,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     P.off_pp = o, o = align(o + P.pp.size() * sizeof(MulPPTask));
     P.off_lists = o, o = align(o + P.lists.size() * 4);
     P.off_prod = o, o = align(o + P.prod.size() * sizeof(MulProdTask));
-    P.off_rows = o, o = align(o + P.row_tasks.size() * sizeof(MulProdTask));
+    P.off_rows = o, o = align(o + P.row_recs.size() * sizeof(MulSpanRec));
     P.off_tiles = o, o = align(o + P.tiles.size() * sizeof(MulTile));
     P.off_res = o, o = align(o + P.res_slots.size() * 4);
     P.off_mspans = o, o = align(o + P.mspans.size() * sizeof(MulTile));
@@ -572,7 +578,7 @@ hm_status upload_plan(hm_ctx *c, MulPlan &P) {
     put(P.off_pp, P.pp.data(), P.pp.size() * sizeof(MulPPTask));
     put(P.off_lists, P.lists.data(), P.lists.size() * 4);
     put(P.off_prod, P.prod.data(), P.prod.size() * sizeof(MulProdTask));
-    put(P.off_rows, P.row_tasks.data(), P.row_tasks.size() * sizeof(MulProdTask));
+    put(P.off_rows, P.row_recs.data(), P.row_recs.size() * sizeof(MulSpanRec));
     put(P.off_tiles, P.tiles.data(), P.tiles.size() * sizeof(MulTile));
     put(P.off_res, P.res_slots.data(), P.res_slots.size() * 4);
     put(P.off_mspans, P.mspans.data(), P.mspans.size() * sizeof(MulTile));
@@ -828,9 +834,9 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
             if (launch_mul_scan(sc, c->stream)) return hip_fail(c, hipGetLastError());
             if (col.nrows) {
                 MulRowArgs ra{};
-                ra.B = B, ra.tasks = (const MulProdTask *)(T + P->off_rows) + col.rows;
+                ra.B = B, ra.recs = (const MulSpanRec *)(T + P->off_rows) + col.rows;
                 ra.ntasks = col.nrows, ra.uw = col.rows_uw, ra.vw = col.rows_vw, ra.ow = col.rows_ow;
-                ra.wave_words = col.nrows * (ra.uw + ra.vw + ra.ow + 2);
+                ra.wave_words = col.nrows * (ra.uw + ra.vw + ra.ow + 2 + 6);
                 if (launch_mul_rows(ra, c->stream)) return hip_fail(c, hipGetLastError());
             }
             for (const MfLaunch &m : col.mfl)
