@@ -324,6 +324,7 @@ struct MulRowArgs {
                             // u words | v words << 16 (slot capacities)
     uint32_t ntasks;
     uint32_t uw, vw, ow;      // LDS words per task's u, v and product (slot capacities)
+    uint32_t qw;              // rows per task: the widest u's words at its degree bound (<= uw)
     uint32_t wave_words;
 };
 constexpr uint32_t kKaNone = 0xFFFFFFFFu; // a z1 that is null (the high halves were all zero)

@@ -72,7 +72,94 @@ __global__ void __launch_bounds__(256) mul_stage_kernel(MulStageArgs S) {
     stage_one(S.B, A.limbs + ge * A.stride + off, rfl(A.degree[ge * A.dstride + j]), bd.b[j], t, e);
 }
 
+// The same staging with one wave per VALUE: lanes over (input bit, limb pair of its slot), so a
+// u8 multiply's 16 bits take two passes of one wave instead of 16 one-pass waves (the per-bit
+// form is latency-bound: 110 us per 16384 u8 pairs).  Per-bit tables in the wave's LDS: slot
+// offset / words, limb offset / capacity in the value, degree, and the OR of its bad flags and its
+// word 0 (ds_or) -- the bounds come in through arg_to_lds (never indexed per lane).
+// LDS per wave: kStageTab * 2K words.
+constexpr uint32_t kStageTab = 8;
+__global__ void __launch_bounds__(256) mul_stage_value_kernel(MulStageArgs S) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t wave = rfl(threadIdx.x >> 6);
+    const uint64_t e = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint32_t lane = (uint32_t)lane_id(), nb = 2 * S.K;
+    uint32_t *tab = lds + (size_t)wave * kStageTab * nb;
+    uint32_t *bnd = tab, *loff = tab + nb, *soff = tab + 2 * nb, *sw = tab + 3 * nb;
+    uint32_t *dg = tab + 4 * nb, *badw = tab + 5 * nb, *w0 = tab + 6 * nb;
+    // (bounds 16-byte aligned for arg_to_lds: nb words each, written up to a multiple of 16)
+    __shared__ __attribute__((aligned(16))) uint32_t sb[4][2 * HM_MAX_BITS];
+    arg_to_lds(S.ab.b, S.K, sb[wave]);
+    arg_to_lds(S.bb.b, S.K, sb[wave] + HM_MAX_BITS);
+    wsync();
+    if (e >= S.B.nv) return; // whole wave exits together (after its LDS writes: no barrier below)
+    const uint64_t ge = S.B.e0 + e;
+    for (uint32_t t = lane; t < nb; t += kWave) {
+        const bool isb = t >= S.K;
+        const uint32_t j = isb ? t - S.K : t;
+        const uint32_t *bd = sb[wave] + (isb ? HM_MAX_BITS : 0);
+        uint32_t off = 0;
+        for (uint32_t q = 0; q < j; ++q) off += cap_of(bd[q]);
+        bnd[t] = bd[j], loff[t] = off;
+        const MulSlot sl = S.B.slots[t];
+        soff[t] = sl.off, sw[t] = sl.words;
+        dg[t] = isb ? S.b.degree[ge * S.b.dstride + j] : S.a.degree[ge * S.a.dstride + j];
+        badw[t] = 0u, w0[t] = 0u;
+    }
+    wsync();
+    uint32_t *dst0 = S.B.arena + e * S.B.astride;
+    // lanes over (bit t, limb g): the slot's (words + 1) / 2 limb pairs, and every limb up to the
+    // bit's capacity (limbs past the slot must be zero, as stage_one checks)
+    uint32_t maxp = 0;
+    for (uint32_t t = 0; t < nb; ++t) maxp = max(maxp, max((sw[t] + 1) / 2, cap_of(bnd[t])));
+    for (uint32_t f = lane; f < nb * maxp; f += kWave) {
+        const uint32_t t = f / maxp, g = f % maxp;
+        const uint32_t bound = bnd[t], deg = dg[t], words = sw[t], cap = cap_of(bound);
+        const bool isb = t >= S.K;
+        const uint64_t *src = (isb ? S.b.limbs : S.a.limbs) + ge * (isb ? S.b.stride : S.a.stride) + loff[t];
+        bool bad = deg > bound;
+        const uint32_t nl = bad ? 0u : deg / 64 + 1, tb = deg % 64;
+        uint64_t v = g < cap ? src[g] : 0ull;
+        if (2 * g < words) {
+            if (g >= nl) {
+                bad |= v != 0;
+                v = 0;
+            } else if (g == nl - 1) {
+                const uint64_t keep = (~0ull) >> (63 - tb);
+                bad |= (v & ~keep) != 0;
+                v &= keep;
+                if (deg > 0 && !((v >> tb) & 1ull)) bad = true;
+            }
+            uint32_t *dst = dst0 + soff[t];
+            dst[2 * g] = (uint32_t)v;
+            if (2 * g + 1 < words) dst[2 * g + 1] = (uint32_t)(v >> 32);
+            if (g == 0) w0[t] = (uint32_t)v; // (one lane per bit)
+        } else if (g < cap) {
+            bad |= v != 0; // a limb past the slot's capacity must be zero
+        }
+        if (bad) atomicOr(&badw[t], 1u);
+    }
+    wsync();
+    bool anybad = false;
+    for (uint32_t t = lane; t < nb; t += kWave) {
+        const bool bad = badw[t] != 0 || dg[t] > bnd[t];
+        anybad |= bad;
+        const bool null = dg[t] == 0 && !(w0[t] & 1u);
+        S.B.deg1[(uint64_t)t * S.B.nv + e] = (bad || null) ? 0u : dg[t] + 1;
+    }
+    if (__any(anybad) && lane == 0) flag(S.B.status, HM_ERR_BAD_INPUT);
+}
+
+#ifndef HM_STAGE_VALUE
+#define HM_STAGE_VALUE 1 // (A/B knob) 0: one wave per (value, input bit)
+#endif
 int launch_mul_stage(const MulStageArgs &S, void *stream) {
+    if (HM_STAGE_VALUE && 2 * S.K <= 64) {
+        if (!S.B.nv) return 0;
+        hipLaunchKernelGGL(mul_stage_value_kernel, dim3((unsigned)((S.B.nv + 3) / 4)), dim3(256),
+                           (size_t)kStageTab * 2 * S.K * 4 * 4, (hipStream_t)stream, S);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     const uint64_t waves = S.B.nv * 2 * S.K;
     if (!waves) return 0;
     hipLaunchKernelGGL(mul_stage_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
@@ -199,8 +286,8 @@ __global__ void __launch_bounds__(256) mul_rows_kernel(MulRowArgs P) {
         W[f] = v;
     }
     wsync();
-    for (uint32_t f = lane; f < P.ntasks * P.uw; f += kWave) {
-        const uint32_t t = f / P.uw, q = f % P.uw;
+    for (uint32_t f = lane; f < P.ntasks * P.qw; f += kWave) {
+        const uint32_t t = f / P.qw, q = f % P.qw;
         uint32_t *Tw = W + t * tw;
         const int nu = bitwords((int)Tw[tw - 2]), nv = bitwords((int)Tw[tw - 1]);
         if ((int)q < nu && nv) clmul_row_xor(Tw[q], Tw + P.uw, nv, Tw + P.uw + P.vw + q);

@@ -101,7 +101,7 @@ struct MulPlan {
         uint32_t tiles[kNW], ntiles[kNW]; // MulTile offsets (in tiles) / counts per width class
         MfLaunch mfl[3];                  // MFMA schoolbook products: tiny, narrow, wide
         uint32_t rows = 0, nrows = 0;     // ... small ones on the VALU by rows (row_tasks range)
-        uint32_t rows_uw = 0, rows_vw = 0, rows_ow = 0;
+        uint32_t rows_uw = 0, rows_vw = 0, rows_ow = 0, rows_qw = 0;
         std::vector<KaProg> ka;           // this column's Karatsuba products
     };
     std::vector<Col> cols;
@@ -243,7 +243,10 @@ bool build_plan(MulPlan &P) {
     enum { IN, PP, PRE, CA, CB, KA, PPA, KA2, NREG };
     Region reg[NREG];
     std::vector<uint8_t> slot_reg;
+    std::vector<int64_t> slot_bnd; // each slot's degree bound
+    auto slot_bound = [&](uint32_t s) { return std::max<int64_t>(slot_bnd[s], 0); };
     auto new_slot = [&](int r, int64_t bound) -> uint32_t {
+        slot_bnd.push_back(bound);
         const uint32_t w = bound < 0 ? 0u : slot_words(bound);
         P.slots.push_back({(uint32_t)reg[r].used, w});
         slot_reg.push_back((uint8_t)r);
@@ -455,6 +458,7 @@ bool build_plan(MulPlan &P) {
         for (uint32_t k = col.prod; k < P.prod.size(); ++k)
             if (rows_ok(k)) {
                 col.rows_uw = std::max(col.rows_uw, P.slots[P.prod[k].u].words);
+                col.rows_qw = std::max(col.rows_qw, (uint32_t)(slot_bound(P.prod[k].u) / 32 + 1));
                 col.rows_vw = std::max(col.rows_vw, P.slots[P.prod[k].v].words);
                 col.rows_ow = std::max(col.rows_ow, P.slots[P.prod[k].out].words);
                 ++col.nrows;
@@ -836,6 +840,7 @@ hm_status mul_columns(hm_ctx *c, const hm_batch *a, const hm_batch *b, uint32_t 
                 MulRowArgs ra{};
                 ra.B = B, ra.recs = (const MulSpanRec *)(T + P->off_rows) + col.rows;
                 ra.ntasks = col.nrows, ra.uw = col.rows_uw, ra.vw = col.rows_vw, ra.ow = col.rows_ow;
+                ra.qw = std::min(col.rows_qw, col.rows_uw);
                 ra.wave_words = col.nrows * (ra.uw + ra.vw + ra.ow + 2 + 6);
                 if (launch_mul_rows(ra, c->stream)) return hip_fail(c, hipGetLastError());
             }
