@@ -500,6 +500,18 @@ hm_status hm_ctx_set_kernel_timing(hm_ctx *c, int enable) try {
     return HM_OK;
 } HM_ABI_CATCH
 
+hm_status hm_ctx_clear_kernel_timing(hm_ctx *c) try {
+    if (!c) return HM_ERR_INVALID_ARGUMENT;
+    if (!c->d_kt) return HM_OK;
+    DeviceGuard g(c->device);
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    const size_t half = (size_t)kTimedLaunches * kTimerWaves * sizeof(unsigned long long);
+    HM_HIP(c, hipMemsetAsync(c->d_kt, 0xFF, half, c->stream));
+    HM_HIP(c, hipMemsetAsync((char *)c->d_kt + half, 0, half, c->stream));
+    HM_HIP(c, hipStreamSynchronize(c->stream));
+    return HM_OK;
+} HM_ABI_CATCH
+
 hm_status hm_ctx_kernel_timing(hm_ctx *c, double *total_ms, uint32_t *launches) try {
     if (!c || !total_ms || !launches) return HM_ERR_INVALID_ARGUMENT;
     *total_ms = 0.0, *launches = 0;

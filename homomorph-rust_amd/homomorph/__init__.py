@@ -457,10 +457,15 @@ class Context:
     def set_kernel_timing(self, enable: bool = True, kernel: str = "add_chain"):
         """hm_ctx_set_kernel_timing: time the launches of `kernel` ("add_chain": the adder's
         carry chain, "encrypt", "decrypt") made or captured from now on (one record slot each,
-        up to 128; a captured launch's slot holds its last replay) by device wall-clock stamps;
-        kernel_timing() reads them back.  Resets the record."""
+        up to 128; a captured launch's slot is valid for one replay, see clear_kernel_timing)
+        by device wall-clock stamps; kernel_timing() reads them back.  Resets the record."""
         k = self.TIMED_KERNELS[kernel] if enable else 0
         _check(lib().hm_ctx_set_kernel_timing(self._h, k), "hm_ctx_set_kernel_timing")
+
+    def clear_kernel_timing(self):
+        """hm_ctx_clear_kernel_timing: clear every slot's stamps, keeping the slots, so that the
+        next replay of a graph captured under timing can be read on its own."""
+        _check(lib().hm_ctx_clear_kernel_timing(self._h), "hm_ctx_clear_kernel_timing")
 
     def kernel_timing(self):
         """(summed kernel ms, launches) of the timed kernel since set_kernel_timing."""

@@ -77,6 +77,7 @@ SIGNATURES = {
     "hm_ctx_set_mul_products": (ctypes.c_int, [vp, ctypes.c_uint32]),
     "hm_ctx_set_add_pipeline": (ctypes.c_int, [vp, ctypes.c_int]),
     "hm_ctx_set_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+    "hm_ctx_clear_kernel_timing": (ctypes.c_int, [vp]),
     "hm_ctx_kernel_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u32p]),
     "hm_fresh_bound": (ctypes.c_uint32, [vp]),
     "hm_add_out_bounds": (ctypes.c_int, [ctypes.c_uint32, u32p, u32p, u32p]),

@@ -199,6 +199,9 @@ hm_status hm_ctx_set_add_pipeline(hm_ctx *ctx, int enable);
  * across replays and nothing clears it in between: the stamps are valid for ONE replay of the
  * graph (R replays make each slot span from the first replay's start to the last one's end).  So
  * enable, capture a K-step graph, replay it once, read: K launches (as the bench times it).
+ * hm_ctx_clear_kernel_timing synchronizes the stream and clears the stamps of every slot while
+ * keeping the slots (and the kernel timed): a graph captured earlier can then be replayed again
+ * and read for that one replay.
  * hm_ctx_kernel_timing synchronizes the stream and returns the summed duration (earliest wave
  * start to latest wave end, per slot) of the launches recorded and their number.
  * HM_TIME_ADD_CHAIN = 1 (hm_add_batch's carry chain, the dominant kernel of the add),
@@ -206,6 +209,7 @@ hm_status hm_ctx_set_add_pipeline(hm_ctx *ctx, int enable);
  * hm_decrypt_batch's kernel. */
 enum { HM_TIME_OFF = 0, HM_TIME_ADD_CHAIN = 1, HM_TIME_ENCRYPT = 2, HM_TIME_DECRYPT = 3 };
 hm_status hm_ctx_set_kernel_timing(hm_ctx *ctx, int kernel);
+hm_status hm_ctx_clear_kernel_timing(hm_ctx *ctx);
 hm_status hm_ctx_kernel_timing(hm_ctx *ctx, double *total_ms, uint32_t *launches);
 
 /* Context::validate_operation (src/context.rs:310-323): HM_OK or HM_ERR_INVALID_PARAMETERS with

@@ -218,6 +218,14 @@ def test_kernel_timing_counts_direct_and_graph_launches(H):
     g.replay()
     ms2, n = ctx.kernel_timing()
     assert n == 3 and ms2 > ms1
+    # hm_ctx_clear_kernel_timing: the slots stay, the stamps go; the next replay reads alone
+    ctx.clear_kernel_timing()
+    ev0.record(ctx.stream)
+    g.replay()
+    ev1.record(ctx.stream)
+    ms3, n = ctx.kernel_timing()
+    torch.cuda.synchronize()
+    assert n == 3 and 0 < ms3 <= ev0.elapsed_time(ev1)
     got = ctx.decrypt(out, np.uint32)
     assert np.array_equal(got, (a + (a ^ 0xFFFF)).astype(np.uint32))
     ctx.set_kernel_timing(True, "encrypt")
