@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 4 /* 4: kernel timing by device stamps (HM_TIME_*), hm_ctx_last_hip_error */
+#define HM_ABI_VERSION 5 /* 4: kernel timing by device stamps (HM_TIME_*), hm_ctx_last_hip_error;
+                            5: hm_ctx_clear_kernel_timing */
 #define HM_MAX_BITS 128 /* u128 is the widest type with impls (src/impls/numbers/uint.rs:58) */
 
 typedef enum hm_status {
