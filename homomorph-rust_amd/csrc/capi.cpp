@@ -554,6 +554,12 @@ hm_status hm_ctx_set_mul_options(hm_ctx *c, uint32_t ka_min, uint32_t ka_leaf) t
     return HM_OK;
 } HM_ABI_CATCH
 
+hm_status hm_ctx_set_mul_scratch(hm_ctx *c, uint64_t words) try {
+    if (!c || words == 0 || words > (1ull << 27) + (1ull << 26)) return HM_ERR_INVALID_ARGUMENT;
+    c->ka_scratch = words;
+    return HM_OK;
+} HM_ABI_CATCH
+
 hm_status hm_ctx_set_add_pipeline(hm_ctx *c, int enable) try {
     if (!c) return HM_ERR_INVALID_ARGUMENT;
     c->add_pipe = enable != 0;

@@ -11,6 +11,9 @@
 
 namespace hm {
 struct MulPlan; // mul_host.cpp
+// default Karatsuba scratch limit, words per value and lane (hm_ctx_set_mul_scratch): above it a
+// product is planned one subtree at a time (mul_host.cpp); every K <= 20 plan stays below it
+constexpr uint64_t kKaScratchWords = 200000000u;
 }
 
 struct hm_ctx {
@@ -74,6 +77,9 @@ struct hm_ctx {
     // Karatsuba carry products (hm_ctx_set_mul_options): shorter operand >= ka_min words (0 =
     // never), recursion down to leaves of at most ka_leaf words
     uint32_t ka_min = 256, ka_leaf = 256;
+    // Karatsuba scratch per value and lane above which a product is planned one subtree at a
+    // time (hm_ctx_set_mul_scratch; mul_host.cpp kKaScratchWords)
+    uint64_t ka_scratch = hm::kKaScratchWords;
     // where the Karatsuba leaf products run (hm_ctx_set_mul_products): HM_MUL_PRODUCTS_*
     uint32_t mul_products = 0;
     // carry chain of the adder (hm_ctx_set_add_options): HM_ADD_CHAIN_AUTO / _MFMA / _VALU

@@ -16,6 +16,8 @@
 #include <array>
 #include <cmath>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <memory>
 
 #include "ctx.h"
@@ -66,6 +68,7 @@ struct KaProg {
     uint32_t leaf_umax = 0, leaf_vmax = 0, leaf_omax = 0; // their largest operands and output
     uint32_t tiles[kNW] = {}, ntiles[kNW] = {};  // their tiles (MulVTile ranges) per width class
     std::vector<std::array<uint32_t, 3>> combs;  // per level k..1: (first KaComb, count, h)
+    bool deg = true; // then the product's exact degree (false: a subtree of a split product)
 };
 
 // One launch of MFMA products (mul_mfma_kernel<false>): spans of `span` output tiles, the LDS
@@ -83,6 +86,7 @@ struct MulPlan {
     uint32_t L = 0, K = 0;
     bool is_signed = false;
     uint32_t ka_min = 0, ka_leaf = 0;           // Karatsuba options (hm_ctx_set_mul_options)
+    uint64_t ka_scratch = 0;                    // ... and hm_ctx_set_mul_scratch
     bool mfma = false;                          // products on the matrix cores (hm_ctx_set_mul_products)
     std::vector<uint32_t> ab, bb;
     // geometry
@@ -232,7 +236,61 @@ struct KaBuild {
         if (combs.size() <= lvl) combs.resize(lvl + 1);
         combs[lvl].push_back({z0, z1, z2, r, rcap});
     }
+
+    // The root of node(0, ...) without its recursion, for a product planned one subtree at a time:
+    // the root's operand sums (sums[0]; always formed, the children are not leaves), its z buffers
+    // and its recombination (combs[0]).  Returns the children, each to be planned into its z
+    // (2h words) with scratch above this builder's top.
+    struct Child {
+        uint32_t uo, un, vo, vn, z;
+    };
+    std::vector<Child> split(uint32_t uo, uint32_t un, uint32_t vo, uint32_t vn, uint32_t n,
+                             uint32_t r, uint32_t rcap) {
+        const uint32_t h = n / 2;
+        std::vector<Child> ch;
+        combs.resize(1);
+        if (un <= h && vn <= h) {
+            const uint32_t z0 = alloc(2 * h);
+            ch.push_back({uo, un, vo, vn, z0});
+            combs[0].push_back({z0, kKaNone, z0, r, rcap});
+            return ch;
+        }
+        struct Half {
+            uint32_t lo_n, hi_o, hi_n, s_o, s_n;
+        };
+        auto half = [&](uint32_t o, uint32_t len) {
+            Half x;
+            x.lo_n = std::min(len, h);
+            x.hi_o = o + h;
+            x.hi_n = len > h ? len - h : 0u;
+            if (x.hi_n == 0) {
+                x.s_o = o, x.s_n = x.lo_n;
+            } else {
+                x.s_o = alloc(h), x.s_n = h;
+                sums.resize(1);
+                sums[0].push_back({o, len, x.s_o});
+            }
+            return x;
+        };
+        const Half U = half(uo, un), V = half(vo, vn);
+        const bool has_z1 = U.hi_n && V.hi_n;
+        const uint32_t z0 = alloc(2 * h), z2 = alloc(2 * h);
+        const uint32_t z1 = has_z1 ? alloc(2 * h) : kKaNone;
+        ch.push_back({uo, U.lo_n, vo, V.lo_n, z0});
+        if (has_z1) ch.push_back({U.hi_o, U.hi_n, V.hi_o, V.hi_n, z1});
+        ch.push_back({U.s_o, U.s_n, V.s_o, V.s_n, z2});
+        combs[0].push_back({z0, z1, z2, r, rcap});
+        return ch;
+    }
 };
+
+// A Karatsuba product whose breadth-first recursion needs more scratch than kKaScratchWords (words
+// per value, per lane) is planned one subtree at a time: the root's sums and z buffers, then each
+// child's own program above them (one after another on the lane's stream, reusing the same
+// scratch), then the root's recombination -- recursively.  The planning views hold 28-bit word
+// offsets per region, so a breadth-first K = 21 product (3.1e8 words) cannot be planned whole;
+// K <= 20 (1.94e8 at most) keeps its one-program plans.
+// (The limit is the context's ka_scratch, hm_ctx_set_mul_scratch; default kKaScratchWords, ctx.h.)
 
 } // namespace
 
@@ -398,47 +456,96 @@ bool build_plan(MulPlan &P) {
             // two lanes (kKaLanes): products alternate between two scratch regions, so that
             // mul_columns can run consecutive products on two streams
             const uint32_t lane = kKaLanes > 1 ? (nka++ & 1u) : 0u;
-            KaBuild kb{(uint32_t)(lane ? KA2 : KA), leaf};
-            kb.fuse_leaf_sums = P.mfma && kFuseLeafSums;
+            const uint32_t region = lane ? KA2 : KA;
             auto view = [&](uint32_t slot) {
                 return ((uint32_t)slot_reg[slot] << kRegShift) | P.slots[slot].off;
             };
-            kb.node(0, view(T.u), nu, view(T.v), nv, leaf << lk, view(T.out), P.slots[T.out].words);
-            reg[lane ? KA2 : KA].max = std::max(reg[lane ? KA2 : KA].max, kb.max);
-            KaProg pg;
-            pg.u = T.u, pg.v = T.v, pg.out = T.out;
-            pg.lane = lane;
-            for (uint32_t l = 0; l < kb.sums.size(); ++l) {
-                if (kb.sums[l].empty()) continue;
-                pg.sums.push_back({(uint32_t)P.ka_sums.size(), (uint32_t)kb.sums[l].size(),
-                                   (leaf << lk) >> (l + 1)});
-                P.ka_sums.insert(P.ka_sums.end(), kb.sums[l].begin(), kb.sums[l].end());
-            }
-            pg.vtask = (uint32_t)P.ka_vtasks.size(), pg.nvtask = (uint32_t)kb.leaves.size();
-            for (const MulVTask &t : kb.leaves) {
-                pg.leaf_umax = std::max(pg.leaf_umax, t.nu);
-                pg.leaf_vmax = std::max(pg.leaf_vmax, t.nv);
-                pg.leaf_omax = std::max(pg.leaf_omax, t.nout);
-            }
-            P.ka_vtasks.insert(P.ka_vtasks.end(), kb.leaves.begin(), kb.leaves.end());
-            uint32_t wc = kNW - 1;
-            for (uint32_t q = 0; q < kNW; ++q)
-                if (kMulTileW[q] * 64 >= 2 * leaf) {
-                    wc = q;
-                    break;
+            // one program from a builder rooted at size n: its sums by depth, its leaves, its
+            // recombinations bottom-up (deg: the product's exact degree after them)
+            auto push_prog = [&](const KaBuild &kb, uint32_t n, bool deg) {
+                KaProg pg;
+                pg.u = T.u, pg.v = T.v, pg.out = T.out;
+                pg.lane = lane;
+                pg.deg = deg;
+                for (uint32_t l = 0; l < kb.sums.size(); ++l) {
+                    if (kb.sums[l].empty()) continue;
+                    pg.sums.push_back({(uint32_t)P.ka_sums.size(), (uint32_t)kb.sums[l].size(), n >> (l + 1)});
+                    P.ka_sums.insert(P.ka_sums.end(), kb.sums[l].begin(), kb.sums[l].end());
                 }
-            pg.tiles[wc] = (uint32_t)P.ka_vtiles.size();
-            for (uint32_t t = 0; t < pg.nvtask; ++t)
-                for (uint32_t b0 = 0; b0 < 2 * leaf; b0 += 64 * kMulTileW[wc])
-                    P.ka_vtiles.push_back({t, b0});
-            pg.ntiles[wc] = (uint32_t)P.ka_vtiles.size() - pg.tiles[wc];
-            for (uint32_t l = (uint32_t)kb.combs.size(); l-- > 0;) {
-                if (kb.combs[l].empty()) continue;
-                pg.combs.push_back({(uint32_t)P.ka_combs.size(), (uint32_t)kb.combs[l].size(),
-                                    (leaf << lk) >> (l + 1)});
-                P.ka_combs.insert(P.ka_combs.end(), kb.combs[l].begin(), kb.combs[l].end());
-            }
-            col.ka.push_back(std::move(pg));
+                pg.vtask = (uint32_t)P.ka_vtasks.size(), pg.nvtask = (uint32_t)kb.leaves.size();
+                for (const MulVTask &t : kb.leaves) {
+                    pg.leaf_umax = std::max(pg.leaf_umax, t.nu);
+                    pg.leaf_vmax = std::max(pg.leaf_vmax, t.nv);
+                    pg.leaf_omax = std::max(pg.leaf_omax, t.nout);
+                }
+                P.ka_vtasks.insert(P.ka_vtasks.end(), kb.leaves.begin(), kb.leaves.end());
+                uint32_t wc = kNW - 1;
+                for (uint32_t q = 0; q < kNW; ++q)
+                    if (kMulTileW[q] * 64 >= 2 * leaf) {
+                        wc = q;
+                        break;
+                    }
+                pg.tiles[wc] = (uint32_t)P.ka_vtiles.size();
+                for (uint32_t t = 0; t < pg.nvtask; ++t)
+                    for (uint32_t b0 = 0; b0 < 2 * leaf; b0 += 64 * kMulTileW[wc])
+                        P.ka_vtiles.push_back({t, b0});
+                pg.ntiles[wc] = (uint32_t)P.ka_vtiles.size() - pg.tiles[wc];
+                for (uint32_t l = (uint32_t)kb.combs.size(); l-- > 0;) {
+                    if (kb.combs[l].empty()) continue;
+                    pg.combs.push_back({(uint32_t)P.ka_combs.size(), (uint32_t)kb.combs[l].size(), n >> (l + 1)});
+                    P.ka_combs.insert(P.ka_combs.end(), kb.combs[l].begin(), kb.combs[l].end());
+                }
+                reg[region].max = std::max(reg[region].max, kb.max);
+                col.ka.push_back(std::move(pg));
+            };
+            // the scratch words KaBuild::node allocates for a (n, un, vn) node, without building it
+            // (the same recursion, memoised: few distinct operand lengths per depth)
+            const bool fuse = P.mfma && kFuseLeafSums;
+            std::map<std::array<uint32_t, 3>, uint64_t> memo;
+            std::function<uint64_t(uint32_t, uint32_t, uint32_t)> scratch = [&](uint32_t n, uint32_t un,
+                                                                               uint32_t vn) -> uint64_t {
+                if (n == leaf) return 0;
+                const auto key = std::array<uint32_t, 3>{n, un, vn};
+                if (auto it = memo.find(key); it != memo.end()) return it->second;
+                const uint32_t h = n / 2;
+                uint64_t s;
+                if (un <= h && vn <= h) {
+                    s = 2ull * h + scratch(h, un, vn);
+                } else {
+                    const uint32_t ulo = std::min(un, h), uhi = un > h ? un - h : 0u;
+                    const uint32_t vlo = std::min(vn, h), vhi = vn > h ? vn - h : 0u;
+                    const bool formed = !(fuse && h == leaf);
+                    s = 4ull * h + (uhi && vhi ? 2ull * h : 0) + (formed && uhi ? h : 0) + (formed && vhi ? h : 0);
+                    s += scratch(h, ulo, vlo) + (uhi && vhi ? scratch(h, uhi, vhi) : 0) +
+                         scratch(h, uhi ? h : ulo, vhi ? h : vlo);
+                }
+                memo[key] = s;
+                return s;
+            };
+            // u * v (views, logical size n) into r; scratch from `top` up (see kKaScratchWords)
+            std::function<void(uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                               uint64_t, bool)>
+                plan_ka = [&](uint32_t uo, uint32_t un, uint32_t vo, uint32_t vn, uint32_t n,
+                              uint32_t r, uint32_t rcap, uint64_t top, bool deg) {
+                    if (scratch(n, std::min(un, n), std::min(vn, n)) <= P.ka_scratch || n <= 2 * leaf) {
+                        KaBuild kb{region, leaf};
+                        kb.fuse_leaf_sums = fuse;
+                        kb.top = kb.max = top;
+                        kb.node(0, uo, un, vo, vn, n, r, rcap);
+                        return push_prog(kb, n, deg);
+                    }
+                    KaBuild rb{region, leaf};
+                    rb.top = rb.max = top;
+                    const std::vector<KaBuild::Child> ch = rb.split(uo, un, vo, vn, n, r, rcap);
+                    KaBuild rs = rb; // the root's sums first (no leaves, no recombination)
+                    rs.combs.clear();
+                    push_prog(rs, n, false);
+                    for (const KaBuild::Child &x : ch)
+                        plan_ka(x.uo, x.un, x.vo, x.vn, n / 2, x.z, n, rb.top, false);
+                    rb.sums.clear(); // ... and its recombination last
+                    push_prog(rb, n, deg);
+                };
+            plan_ka(view(T.u), nu, view(T.v), nv, leaf << lk, view(T.out), P.slots[T.out].words, 0, true);
             is_ka[k - col.prod] = true;
         }
         // tiles of this column's schoolbook products: MFMA spans where the uniform operand has
@@ -609,14 +716,14 @@ hm_status get_plan(hm_ctx *c, uint32_t L, uint32_t K, const uint32_t *ab, const 
                    bool is_signed, MulPlan *&out) {
     for (MulPlan *p : c->mul_plans)
         if (p->L == L && p->K == K && p->is_signed == is_signed && p->ka_min == c->ka_min &&
-            p->ka_leaf == c->ka_leaf && p->mfma == mul_on_mfma(c) &&
+            p->ka_leaf == c->ka_leaf && p->ka_scratch == c->ka_scratch && p->mfma == mul_on_mfma(c) &&
             std::equal(p->ab.begin(), p->ab.end(), ab) && std::equal(p->bb.begin(), p->bb.end(), bb)) {
             out = p;
             return HM_OK;
         }
     auto P = std::make_unique<MulPlan>();
     P->L = L, P->K = K, P->is_signed = is_signed;
-    P->ka_min = c->ka_min, P->ka_leaf = c->ka_leaf;
+    P->ka_min = c->ka_min, P->ka_leaf = c->ka_leaf, P->ka_scratch = c->ka_scratch;
     P->mfma = mul_on_mfma(c);
     P->ab.assign(ab, ab + K), P->bb.assign(bb, bb + K);
     if (!build_plan(*P)) return HM_ERR_UNSUPPORTED;
@@ -713,7 +820,9 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         a.B = B, a.t = (const KaSum *)(T + P.off_ka_sums) + lv[0], a.nt = lv[1], a.h = lv[2];
         if (launch_ka_sum(a, st)) return hip_fail(c, hipGetLastError());
     }
-    if (P.mfma) {
+    if (!pg.nvtask) {
+        // (a split product's root sums or recombination: no leaves)
+    } else if (P.mfma) {
         // the leaves on the matrix cores: one wave per (value, leaf)
         MulMfmaArgs a{};
         a.B = B, a.tasks = (const MulVTask *)(T + P.off_ka_vtasks) + pg.vtask;
@@ -742,6 +851,7 @@ hm_status run_ka(hm_ctx *c, const MulPlan &P, const KaProg &pg, const MulBase &B
         a.B = B, a.t = (const KaComb *)(T + P.off_ka_combs) + lv[0], a.nt = lv[1], a.h = lv[2];
         if (launch_ka_comb(a, st)) return hip_fail(c, hipGetLastError());
     }
+    if (!pg.deg) return HM_OK;
     MulDegArgs d{};
     d.B = B, d.u = pg.u, d.v = pg.v, d.out = pg.out;
     if (launch_mul_deg(d, st)) return hip_fail(c, hipGetLastError());

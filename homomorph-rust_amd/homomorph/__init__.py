@@ -482,6 +482,12 @@ class Context:
         _check(lib().hm_ctx_set_mul_options(self._h, karatsuba_min_words, karatsuba_leaf_words),
                "hm_ctx_set_mul_options")
 
+    def set_mul_scratch(self, words_per_value: int = 200_000_000):
+        """hm_ctx_set_mul_scratch: the Karatsuba scratch (32-bit words per value and lane) above
+        which a product's recursion is planned one subtree at a time.  Results are identical
+        either way."""
+        _check(lib().hm_ctx_set_mul_scratch(self._h, words_per_value), "hm_ctx_set_mul_scratch")
+
     MUL_PRODUCTS = {"auto": 0, "mfma": 1, "valu": 2}
 
     def set_mul_products(self, products: str = "auto"):

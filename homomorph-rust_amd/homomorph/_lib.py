@@ -73,6 +73,7 @@ SIGNATURES = {
     "hm_ctx_get_public_key": (ctypes.c_int, [vp, u64p, ctypes.c_size_t, u32p, u32p]),
     "hm_validate_operation": (ctypes.c_int, [vp, ctypes.c_int, u16p]),
     "hm_ctx_set_mul_options": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "hm_ctx_set_mul_scratch": (ctypes.c_int, [vp, ctypes.c_uint64]),
     "hm_ctx_set_add_options": (ctypes.c_int, [vp, ctypes.c_uint32]),
     "hm_ctx_set_mul_products": (ctypes.c_int, [vp, ctypes.c_uint32]),
     "hm_ctx_set_add_pipeline": (ctypes.c_int, [vp, ctypes.c_int]),

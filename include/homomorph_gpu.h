@@ -35,7 +35,7 @@ extern "C" {
 #endif
 
 #define HM_ABI_VERSION 5 /* 4: kernel timing by device stamps (HM_TIME_*), hm_ctx_last_hip_error;
-                            5: hm_ctx_clear_kernel_timing */
+                            5: hm_ctx_clear_kernel_timing, hm_ctx_set_mul_scratch */
 #define HM_MAX_BITS 128 /* u128 is the widest type with impls (src/impls/numbers/uint.rs:58) */
 
 typedef enum hm_status {
@@ -161,6 +161,15 @@ hm_status hm_ctx_get_public_key(const hm_ctx *ctx, uint64_t *limbs, size_t cap, 
  * prefixes at d = d' = 128 once the leaves run on the matrix cores; 192 and 192 at d = d' = 256). */
 hm_status hm_ctx_set_mul_options(hm_ctx *ctx, uint32_t karatsuba_min_words,
                                  uint32_t karatsuba_leaf_words);
+/* Karatsuba scratch (no effect on results).  A Karatsuba product's recursion runs breadth-first
+ * (all its leaves in one launch, then the recombinations bottom-up), so every node's buffers are
+ * alive at once and the scratch grows as n^1.585.  A product whose recursion needs more than
+ * words_per_value 32-bit words of scratch per value is planned one subtree at a time instead: the
+ * root's operand sums and child products first, then each child's own recursion (recursively,
+ * reusing the scratch above the root's), then the root's recombination.  Default 2e8 words (every
+ * product up to the u32 multiply's K = 20 prefix runs whole; K = 21..24 need the split).  At most
+ * 2^27 + 2^26 words (the plan's views hold 28-bit offsets); at least 1. */
+hm_status hm_ctx_set_mul_scratch(hm_ctx *ctx, uint64_t words_per_value);
 
 /* Where the multiplier's products run (no effect on results: every product is exact): as {0,1}
  * Toeplitz GEMMs on the fp4 matrix cores (MFMA, reduced mod 2) or as VALU products.  The choice

@@ -278,6 +278,47 @@ def test_mul_low20_karatsuba_vs_schoolbook(H):
     assert_batches_equal(kl, kd, sl, sd, ka.bound, n, "K=20 karatsuba vs schoolbook")
 
 
+def test_mul_karatsuba_split_plans_equal_whole(H):
+    """hm_ctx_set_mul_scratch: with a scratch limit of 2^18 words per value every K = 16 Karatsuba
+    product above it is planned one subtree at a time (root sums and children first, each child's
+    own recursion, the root's recombination last), and the ciphertexts are identical to the
+    breadth-first plans' on 4 values (the K = 16 products need up to 3.2e6 words whole)."""
+    params, n, k = (128, 128, 1, 128), 4, 16
+    ctx = make_ctx(H, params, 141)
+    a, b = plain(n, np.uint32, 142), plain(n, np.uint32, 143)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)
+    whole = ctx.mul_low(ca, cb, k)
+    ctx.synchronize()
+    ctx.set_mul_scratch(1 << 18)
+    split = ctx.mul_low(ca, cb, k)
+    ctx.synchronize()
+    wl, wd = whole.to_host()
+    sl, sd = split.to_host()
+    assert_batches_equal(wl, wd, sl, sd, whole.bound, n, "K=16 split vs whole Karatsuba plans")
+
+
+def test_mul_low22_split_plan(H):
+    """Result bits 20 and 21 of the u32 multiply (K = 22), past the breadth-first planning limit
+    (K = 21 and up need more than the 28-bit views' scratch): the products above
+    hm_ctx_set_mul_scratch's default are planned one subtree at a time.  Under an S(0) = 0 key
+    both values decrypt to a*b mod 2^22, and every output polynomial (17 MB per value) passes the
+    residue check against the reference's circuit."""
+    import torch
+    params, n, k = (128, 128, 1, 128), 2, 22
+    ctx = make_ctx(H, params, _s0_zero_seed(params))
+    a, b = plain(n, np.uint32, 144), plain(n, np.uint32, 145)
+    ca, cb = ctx.encrypt(a), ctx.encrypt(b)
+    cp = ctx.mul_low(ca, cb, k)
+    raw = ctx.decrypt_bytes(H.pad_bits(cp, 24)).cpu().numpy().astype(np.uint64)
+    ctx.synchronize()
+    got = raw[:, 0] | (raw[:, 1] << np.uint64(8)) | (raw[:, 2] << np.uint64(16))
+    want = (a.astype(np.uint64) * b) & np.uint64((1 << k) - 1)
+    assert np.array_equal(got, want), (got, want)
+    assert helpers.check_residues(H, "mul", cp, ca, cb, k=k, seed=146) == n
+    del cp
+    torch.cuda.empty_cache()
+
+
 def test_mixed_config4_full_batch(H, oracle):
     """configs[4] at its full global batch, 2^20 values at d = dp = tau = 256, on one GPU through
     bench.py's own chunk loop (the N = 1 point of the strong-scaling config): every sum and
