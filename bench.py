@@ -775,7 +775,10 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
                         (f"u32_mul_low{MUL_LOW_BENCH}", MUL_LOW_BENCH, MUL_BATCH),
                         (f"u32_mul_low{MUL_LOW_BENCH}_batch{n32}", MUL_LOW_BENCH, n32),
                         ("u32_mul_low20", 20, MUL_BATCH),
-                        ("u32_mul_low20_batch16", 20, 16)):
+                        ("u32_mul_low20_batch16", 20, 16),
+                        # result bits 20..23: products planned one subtree at a time
+                        # (hm_ctx_set_mul_scratch), 2.3 GB of arena and 57e6 leaf products per value
+                        ("u32_mul_low24_batch2", 24, 2)):
         ob = H.mul_out_bounds(c32a.bound[:k], c32b.bound[:k])
         va, vb = H.value_slice(c32a, 0, nk), H.value_slice(c32b, 0, nk)
         cp = H.Ciphered.empty(nk, ob, device)
@@ -808,24 +811,26 @@ def secondary_metrics(ctx, device, steps, add_out, cpu_seconds, cpu_add=None):
             "bit_exact": "tests/test_golden.py (oracle fixtures: K=16, 8 values; K=20, 4 "
                          "values), test_gpu_properties.py (residue check of all 1024 K=16 "
                          "products; K=20 at batch 1024 under an S(0)=0 key: all decrypt, 64 "
-                         "by residue; K=20 Karatsuba = schoolbook), test_gpu_parity.py",
+                         "by residue; K=20 Karatsuba = schoolbook; K=22 split plans: decrypt + "
+                         "residues; split = whole plans at K=16), test_gpu_parity.py",
             "roofline": mul_roofline(mctx, c32a.bound, c32b.bound, k, nk, ev_s / reps,
                                      f"u32 multiply, low {k} bits"),
             "cpu_baseline": cpu_mul_low(k)}
         del cp
     full = H.mul_cost(c32a.bound, c32b.bound)
-    kx = out["u32_mul_low20"]
+    kx = out["u32_mul_low24_batch2"]
     est = kx["word_pairs_per_s"] / full["word_pairs"]
     out["u32_mul_full_extrapolated"] = {
         "value": est * 1.0, "unit": "u32 muls/s (EXTRAPOLATED, not measured)",
-        "basis": "the low-20 rate in word pairs/s (hm_mul_cost) applied to the full circuit's "
-                 "word pairs; the full circuit also needs its outputs and carries resident, "
-                 "which no GPU holds",
+        "basis": "the low-24 rate (the deepest prefix run) in schoolbook word pairs/s (hm_mul_cost) "
+                 "applied to the full circuit's word pairs; the full circuit also needs its "
+                 "outputs and carries resident (8.4 GiB of output per value) and per-leaf task "
+                 "tables that grow 7.4x per 2 result bits (2.3 GB at K = 24)",
         "word_pairs_per_mul": full["word_pairs"], "out_bytes_per_mul": full["out_bytes"],
         "max_degree": full["max_degree"], "seconds_per_mul_one_gpu": 1.0 / est,
-        "roofline": dict(kx["roofline"], note="EXTRAPOLATED: the low-20 multiply's measured "
+        "roofline": dict(kx["roofline"], note="EXTRAPOLATED: the low-24 multiply's measured "
                          "roofline (the rate above is that word-pair rate)"),
-        "cpu_baseline": dict(cpu_mul_low(20), value=k12_pairs_s / full["word_pairs"],
+        "cpu_baseline": dict(cpu_mul_low(24), value=k12_pairs_s / full["word_pairs"],
                              sample=f"EXTRAPOLATED: the K = 12 oracle leg's {k12_pairs_s:.3g} word "
                                     f"pairs/s (1 thread) applied to the full circuit's "
                                     f"{full['word_pairs']:.4g} word pairs")}

@@ -39,7 +39,8 @@ def test_bench_every_line_has_roofline_and_cpu_baseline():
     assert "error" not in sec, sec.get("error")
     for name in ("u32_encrypt_decrypt", "u32_encrypt", "u32_decrypt_fresh", "u32_decrypt_after_add",
                  "u32_add_pcie_inclusive", "u8_mul", "u8_decrypt_after_mul", "u32_mul_low12",
-                 "u32_mul_low16", "u32_mul_low16_batch16384", "u32_mul_low20", "u32_mul_full_extrapolated", "mixed_config4",
+                 "u32_mul_low16", "u32_mul_low16_batch16384", "u32_mul_low20", "u32_mul_low24_batch2",
+                 "u32_mul_full_extrapolated", "mixed_config4",
                  "config0_u8_encrypt", "config0_u8_decrypt", "config0_u8_add"):
         line = sec[name]
         assert line["value"] > 0, name
@@ -59,6 +60,7 @@ def test_bench_every_line_has_roofline_and_cpu_baseline():
     assert sec["u32_mul_low20"]["batch"] == 1024  # result bits 16..19 at configs[3]'s batch
     assert sec["u32_mul_low16_batch16384"]["batch"] == 16384
     assert sec["u32_mul_low20_batch16"]["batch"] == 16
+    assert sec["u32_mul_low24_batch2"]["batch"] == 2  # result bits 20..23 (split plans)
     assert sec["u32_mul_low12"]["cpu_baseline"].get("extrapolated") is None
     m = sec["mixed_config4"]
     assert m["verified"]["correct_sums"] == m["verified"]["correct_products"] == m["global_batch"]

@@ -16,6 +16,9 @@ properties (the oracle alone would take minutes to hours on the whole batches).
   configs[3] u32 mul (low 20 bits), batch 1024        under an S(0) = 0 key every product decrypts
                                                       to a*b mod 2^20, 64 by residue; on two values
                                                       Karatsuba = schoolbook
+  u32 mul (low 22 / 24 bits), 2 / 1 values           split Karatsuba plans: decrypt to a*b mod
+                                                      2^K under an S(0) = 0 key, all by residue;
+                                                      split = whole plans at K = 16
   configs[4] mixed add + mul-low-8, d=dp=tau=256,     the whole 2^20 global batch on one GPU through
              2^20 values                              bench.py's chunk loop: every value decrypts,
                                                       2048 sampled values bit-exact vs the oracle
@@ -297,16 +300,18 @@ def test_mul_karatsuba_split_plans_equal_whole(H):
     assert_batches_equal(wl, wd, sl, sd, whole.bound, n, "K=16 split vs whole Karatsuba plans")
 
 
-def test_mul_low22_split_plan(H):
-    """Result bits 20 and 21 of the u32 multiply (K = 22), past the breadth-first planning limit
+@pytest.mark.parametrize("k,n", [(22, 2), (24, 1)])
+def test_mul_low_deep_split_plan(H, k, n):
+    """Result bits 20..23 of the u32 multiply (K = 22, 24), past the breadth-first planning limit
     (K = 21 and up need more than the 28-bit views' scratch): the products above
-    hm_ctx_set_mul_scratch's default are planned one subtree at a time.  Under an S(0) = 0 key
-    both values decrypt to a*b mod 2^22, and every output polynomial (17 MB per value) passes the
-    residue check against the reference's circuit."""
+    hm_ctx_set_mul_scratch's default are planned one subtree at a time (K = 24: 57e6 leaf
+    products per value, ~1 s).  Under an S(0) = 0 key every value decrypts to a*b mod 2^K, and
+    every output polynomial (17 / 60 MB per value) passes the residue check against the
+    reference's circuit."""
     import torch
-    params, n, k = (128, 128, 1, 128), 2, 22
+    params = (128, 128, 1, 128)
     ctx = make_ctx(H, params, _s0_zero_seed(params))
-    a, b = plain(n, np.uint32, 144), plain(n, np.uint32, 145)
+    a, b = plain(n, np.uint32, 144 + k), plain(n, np.uint32, 145 + k)
     ca, cb = ctx.encrypt(a), ctx.encrypt(b)
     cp = ctx.mul_low(ca, cb, k)
     raw = ctx.decrypt_bytes(H.pad_bits(cp, 24)).cpu().numpy().astype(np.uint64)
