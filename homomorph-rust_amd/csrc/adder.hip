@@ -28,61 +28,89 @@ __device__ __forceinline__ uint32_t limb_off(const Bounds &B, uint32_t i) {
     return o;
 }
 
-// Stage bits [i0, i0+nb) of one value's input (u64 limbs, exact degrees) into LDS words: bit
-// i0+t at dst + t*cnt, its word count at nw[t] (0 = null).  Lanes stride over the range's
-// contiguous limbs (all its bits at once, coalesced); every limb is validated against its bit's
-// degree word as in load_bit.  src/deg point at the value's first limb / degree word.  tb: 2 nb
-// LDS words for the range's bounds and limb end offsets -- the per-lane bit cursor reads them
-// there, never from the by-value Bounds (dev_common.h: by-value argument arrays).
-__device__ __forceinline__ void stage_bits(const uint64_t *__restrict__ src, const uint32_t *__restrict__ deg,
-                           const Bounds &B, uint32_t i0, uint32_t nb, uint32_t *dst, uint32_t cnt,
-                           uint32_t *nw, uint32_t *tb, int *status) {
-    const int lane = lane_id();
+// Validate limb v = limb k of a bit of degree d and bound bnd (as load_bit): limbs above the
+// degree must be zero, the top limb's bits above the degree too, and a nonzero degree's bit must be
+// set; returns the limb masked at the degree (0 for an invalid bit, whose staged words are zeros).
+__device__ __forceinline__ uint64_t checked_limb(uint64_t v, uint32_t d, uint32_t bnd, uint32_t k, bool &bad) {
+    const uint32_t nl = d / 64 + 1;
+    if (d > bnd) {
+        bad = true;
+        return 0; // (every staged word is written: the fixed-length product rows read them all)
+    }
+    if (k >= nl) {
+        bad |= v != 0; // limbs above the degree must be zero (layout invariant)
+        return 0;
+    }
+    if (k == nl - 1) {
+        const uint32_t top = d % 64;
+        const uint64_t keep = (~0ull) >> (63 - top);
+        bad |= (v & ~keep) != 0;
+        v &= keep;
+        if (d > 0 && !((v >> top) & 1ull)) bad = true;
+    }
+    return v;
+}
+
+// Stage bits [i0, i0+nb) of both operands of one value (u64 limbs, exact degrees) into LDS words,
+// validating every limb against its bit's degree word: bit i0+t of a at Al + t*cntA, its word
+// count at nAl[t] (0 = null), of b at Bl + t*cntB / nBl[t].  Lanes stride over each range's
+// contiguous limbs (coalesced).  One global round trip: the bits' degrees (one per lane) and each
+// lane's first limb of both operands are all in flight before the first wait (round 6; the
+// per-operand form waited for limbs, then for degrees, twice).  nAl / nBl hold the degrees until
+// the last pass turns them into word counts.  tb: 4 nb LDS words for both ranges' bounds and limb
+// end offsets -- the per-lane bit cursors read them there, never from the by-value Bounds
+// (dev_common.h: by-value argument arrays).  pa/da, pb/db: the value's first limb / degree word.
+__device__ __forceinline__ void stage_ab(const uint64_t *__restrict__ pa, const uint32_t *__restrict__ da,
+                                         const Bounds &BA, const uint64_t *__restrict__ pb,
+                                         const uint32_t *__restrict__ db, const Bounds &BB, uint32_t i0,
+                                         uint32_t nb, uint32_t *Al, uint32_t cntA, uint32_t *nAl,
+                                         uint32_t *Bl, uint32_t cntB, uint32_t *nBl, uint32_t *tb,
+                                         int *status) {
+    const uint32_t lane = (uint32_t)lane_id();
     i0 = rfl(i0), nb = rfl(nb);
-    src += limb_off(B, i0);
-    deg += i0;
-    uint32_t *bnd = tb, *ends = tb + nb;
-    // uniform pass: bounds and inclusive limb end offsets of the range's bits, scalar reads only
-    uint32_t total = 0, vb = 0, ve = 0;
+    pa += limb_off(BA, i0), pb += limb_off(BB, i0);
+    da += i0, db += i0;
+    uint32_t dga = 0, dgb = 0;
+    if (lane < nb) dga = da[lane], dgb = db[lane];
+    // uniform pass: bounds and inclusive limb end offsets of both ranges, scalar reads only
+    uint32_t tota = 0, totb = 0, vba = 0, vea = 0, vbb = 0, veb = 0;
     for (uint32_t t = 0; t < nb; ++t) {
-        const uint32_t b = B.b[i0 + t];
-        total += cap_of(b);
-        if ((uint32_t)lane == t) vb = b, ve = total;
+        const uint32_t ba = BA.b[i0 + t], bb = BB.b[i0 + t];
+        tota += cap_of(ba), totb += cap_of(bb);
+        if (lane == t) vba = ba, vea = tota, vbb = bb, veb = totb;
     }
-    if ((uint32_t)lane < nb) bnd[lane] = vb, ends[lane] = ve;
+    const uint64_t fa = lane < tota ? pa[lane] : 0ull, fb = lane < totb ? pb[lane] : 0ull;
+    uint32_t *bnda = tb, *enda = tb + nb, *bndb = tb + 2 * nb, *endb = tb + 3 * nb;
+    if (lane < nb) {
+        bnda[lane] = vba, enda[lane] = vea, bndb[lane] = vbb, endb[lane] = veb;
+        nAl[lane] = dga, nBl[lane] = dgb;
+    }
     // slot words past a bit's own capacity (bits of smaller bounds than the slot's) read as zero
-    for (uint32_t k = lane; k < nb * cnt; k += kWave) dst[k] = 0u;
+    for (uint32_t k = lane; k < nb * cntA; k += kWave) Al[k] = 0u;
+    for (uint32_t k = lane; k < nb * cntB; k += kWave) Bl[k] = 0u;
     wsync();
-    uint32_t t = 0, lo = 0, hi = nb ? ends[0] : 0;
     bool bad = false;
-    for (uint32_t g = lane; g < total; g += kWave) {
-        while (g >= hi) ++t, lo = hi, hi = ends[t];
-        const uint32_t d = deg[t], k = g - lo;
-        uint64_t v = src[g];
-        const uint32_t nl = d / 64 + 1;
-        if (d > bnd[t]) {
-            bad = true;
-            v = 0; // (every staged word is written: the fixed-length product rows read them all)
-        } else if (k >= nl) {
-            bad |= v != 0; // limbs above the degree must be zero (layout invariant)
-            v = 0;
-        } else if (k == nl - 1) {
-            const uint32_t top = d % 64;
-            const uint64_t keep = (~0ull) >> (63 - top);
-            bad |= (v & ~keep) != 0;
-            v &= keep;
-            if (d > 0 && !((v >> top) & 1ull)) bad = true;
+    auto one = [&](const uint64_t *src, uint64_t first, uint32_t total, const uint32_t *bnd,
+                   const uint32_t *ends, const uint32_t *deg, uint32_t *dst, uint32_t cnt) {
+        uint32_t t = 0, lo = 0, hi = nb ? ends[0] : 0;
+        for (uint32_t g = lane; g < total; g += kWave) {
+            while (g >= hi) ++t, lo = hi, hi = ends[t];
+            const uint32_t k = g - lo;
+            const uint64_t v = checked_limb(g == lane ? first : src[g], deg[t], bnd[t], k, bad);
+            dst[t * cnt + 2 * k] = (uint32_t)v;
+            dst[t * cnt + 2 * k + 1] = (uint32_t)(v >> 32);
         }
-        dst[t * cnt + 2 * k] = (uint32_t)v;
-        dst[t * cnt + 2 * k + 1] = (uint32_t)(v >> 32);
-    }
+    };
+    one(pa, fa, tota, bnda, enda, nAl, Al, cntA);
+    one(pb, fb, totb, bndb, endb, nBl, Bl, cntB);
     if (__any(bad) && lane == 0) flag(status, HM_ERR_BAD_INPUT);
     wsync();
-    for (uint32_t k = lane; k < nb; k += kWave) {
-        const uint32_t d = deg[k];
-        uint32_t n = d / 32 + 1;
-        if (d > bnd[k] || (d == 0 && !(dst[k * cnt] & 1u))) n = 0;
-        nw[k] = n;
+    if (lane < nb) {
+        const uint32_t d1 = nAl[lane], d2 = nBl[lane];
+        uint32_t n1 = d1 / 32 + 1, n2 = d2 / 32 + 1;
+        if (d1 > bnda[lane] || (d1 == 0 && !(Al[lane * cntA] & 1u))) n1 = 0;
+        if (d2 > bndb[lane] || (d2 == 0 && !(Bl[lane * cntB] & 1u))) n2 = 0;
+        nAl[lane] = n1, nBl[lane] = n2;
     }
 }
 
@@ -102,12 +130,11 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits [i0, i0 + nmine)
     const uint32_t i0 = min(L, part * bpw), nmine = min(L, i0 + bpw) - i0;
     // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][P: bpw cntP][na nb dAB dP]
-    //      [stage_bits' bound / end-offset table: 2 bpw]
+    //      [2 bpw more: with dAB / dP (zeroed after it), stage_ab's bound / end-offset tables]
     uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
     uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
     uint32_t *ABl = Xl + bpw * A.cntX, *Pl = ABl + bpw * A.cntAB;
     uint32_t *nAl = Pl + bpw * A.cntP, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
-    uint32_t *Tb = dP + bpw;
     uint32_t *ws = A.ws + e * A.ws_stride;
     uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
     uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
@@ -115,8 +142,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
 
     // stage + validate this wave's bits (every bit is validated, the last one too)
-    stage_bits(pa, da, A.ab, i0, nmine, Al, A.cntA, nAl, Tb, A.status);
-    stage_bits(pb, db, A.bb, i0, nmine, Bl, A.cntB, nBl, Tb, A.status);
+    stage_ab(pa, da, A.ab, pb, db, A.bb, i0, nmine, Al, A.cntA, nAl, Bl, A.cntB, nBl, dAB, A.status);
     for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
     // products only for bits < L-1 (the last bit has no outgoing carry)

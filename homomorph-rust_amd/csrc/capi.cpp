@@ -802,7 +802,7 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         A.wpv = (uint32_t)std::max<uint64_t>(
             1, std::min<uint64_t>({std::max(want, rows_fit), 8, (uint64_t)L}));
         const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
-        // (+ 2 bpw: stage_bits' per-lane bound / offset table; a wave's range is at most 64 bits)
+        // (+ 2 bpw: with dAB / dP, stage_ab's bound / offset tables; a wave's range is at most 64 bits)
         if (bpw > 64) return HM_ERR_UNSUPPORTED;
         A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 6 * bpw);
         if ((size_t)A.prep_lds * 4 * 4 > 160 * 1024) return HM_ERR_UNSUPPORTED;
