@@ -117,7 +117,9 @@ __device__ __forceinline__ void stage_ab(const uint64_t *__restrict__ pa, const 
 // NB, NAB > 0: the plan's b_i and ab_i slots hold exactly NB and NAB words (d + d' = 128 / 256 /
 // 512: 6 / 10 / 18 and 9 / 17 / 33), and the product rows run at those fixed lengths
 // (clmul_row_xor_fixed: unrolled, zero-padded); 0: lengths from the degrees
-template <int NB, int NAB>
+// TOP1: AddArgs.top1 (the top-word copies below), a separate instance so that the plain one keeps
+// its code (the copies' dead branch cost configs[0]'s prep 1.3 % as a runtime flag)
+template <int NB, int NAB, bool TOP1 = false>
 __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
     const uint32_t wave = rfl(threadIdx.x >> 6);
@@ -160,7 +162,22 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
 
     // Products by rows: lanes over (slot t, multiplier word q) -- every lane of a slot runs the
     // same number of steps (the multiplicand's length), rows meet in LDS through ds_xor.
-    const uint32_t cq = A.cntX; // multiplier words: a_i (phase 1) and x_i (phase 2) fit in cntX
+    // Multiplier words: a_i (phase 1) and x_i (phase 2) fit in cntX.  With top1 their word
+    // cntX - 1 is 0 or 1, so its row is the multiplicand shifted by cntX - 1 words: top_rows adds
+    // it as a copy (ds_xor), and the rows cover words 0 .. cntX - 2 (for_rows).
+    const uint32_t cq = A.cntX - (TOP1 ? 1u : 0u);
+    const uint32_t qt = A.cntX - 1; // (top1) the top word's index
+    auto top_rows = [&](uint32_t cnt, auto &&len, auto &&set, const uint32_t *src, uint32_t scnt,
+                        uint32_t *dst, uint32_t dcnt) {
+        // lanes over (slot t, multiplicand word k): dst_t[qt + k] ^= src_t[k] where the top bit is set
+        const uint32_t dt = kWave / cnt, dk = kWave % cnt;
+        uint32_t t = (uint32_t)lane / cnt, k = (uint32_t)lane % cnt;
+        for (uint32_t f0 = 0; f0 < nprod * cnt; f0 += kWave) {
+            if (t < nprod && k < len(t) && set(t)) atomicXor(&dst[t * dcnt + qt + k], src[t * scnt + k]);
+            t += dt, k += dk;
+            if (k >= cnt) k -= cnt, ++t;
+        }
+    };
     auto for_rows = [&](auto &&row) {
         const uint32_t dt = kWave / cq, dq = kWave % cq;
         uint32_t t = (uint32_t)lane / cq, q = (uint32_t)lane % cq;
@@ -183,6 +200,9 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
             }
         }
     });
+    if constexpr (TOP1) // a_i's word qt is 1 exactly when a_i has cntX words (exact degrees)
+        top_rows(A.cntB, [&](uint32_t t) { return nBl[t]; }, [&](uint32_t t) { return nAl[t] == A.cntX; },
+                 Bl, A.cntB, ABl, A.cntAB);
     wsync();
     for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
         const uint32_t t = f / A.cntAB, m = f % A.cntAB;
@@ -203,6 +223,9 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
             }
         }
     });
+    if constexpr (TOP1) // x_i's word qt (a_i's and b_i's top bits may cancel)
+        top_rows(A.cntAB, [&](uint32_t t) { return (uint32_t)bitwords((int)dAB[t]); },
+                 [&](uint32_t t) { return (Xl[t * A.cntX + qt] & 1u) != 0; }, ABl, A.cntAB, Pl, A.cntP);
     wsync();
     for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) {
         const uint32_t t = f / A.cntP, m = f % A.cntP;
@@ -357,7 +380,9 @@ int launch_add_prep(const AddArgs &a, void *stream) {
 #ifndef HM_PREP_FIXED
 #define HM_PREP_FIXED 0 // (A/B knob) 1: product rows at the slots' fixed lengths (measured neutral, r06)
 #endif
-    if (HM_PREP_FIXED && a.cntB == 10 && a.cntAB == 17)
+    if (a.top1)
+        hipLaunchKernelGGL((add_prep_kernel<0, 0, true>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+    else if (HM_PREP_FIXED && a.cntB == 10 && a.cntAB == 17)
         hipLaunchKernelGGL((add_prep_kernel<10, 17>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
     else if (HM_PREP_FIXED && a.cntB == 6 && a.cntAB == 9)
         hipLaunchKernelGGL((add_prep_kernel<6, 9>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);

@@ -773,12 +773,14 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
 
     // Workspace slots (words) and LDS plans, from the static bounds
     uint32_t cntA = 0, cntB = 0, cntAB = 0, cntP = 0, cntX = 1, SC = 2, maxPw = 0;
+    int64_t maxb = 0; // the largest input bound
     int64_t cb = -1;
     for (uint32_t i = 0; i < L; ++i) {
         const int64_t ba = a->bound[i], bb = b->bound[i];
         cntA = std::max(cntA, 2 * cap_of(a->bound[i]));
         cntB = std::max(cntB, 2 * cap_of(b->bound[i]));
         cntX = std::max(cntX, words_of_bound(std::max(ba, bb)));
+        maxb = std::max(maxb, std::max(ba, bb));
         if (i + 1 < L) {
             const int64_t x = std::max(ba, bb), ab = ba + bb, p = x + ab;
             cntAB = std::max(cntAB, words_of_bound(ab));
@@ -797,10 +799,18 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     // contiguous ranges)
     {
         const uint64_t want = (16384 + a->n - 1) / a->n;
-        const uint64_t rows_fit = (L + std::max<uint32_t>(1, 64 / cntX) - 1) /
-                                  std::max<uint32_t>(1, 64 / cntX);
-        A.wpv = (uint32_t)std::max<uint64_t>(
-            1, std::min<uint64_t>({std::max(want, rows_fit), 8, (uint64_t)L}));
+        auto waves = [&](uint32_t rows) { // rows: product rows per bit
+            const uint64_t rows_fit = (L + std::max<uint32_t>(1, 64 / rows) - 1) /
+                                      std::max<uint32_t>(1, 64 / rows);
+            return (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>({std::max(want, rows_fit), 8, (uint64_t)L}));
+        };
+        // the top word of every a_i, b_i, x_i holds at most bit 32 (cntX - 1) = maxb: the prep can
+        // add its multiples as shifted copies instead of product rows -- worth it when the shorter
+        // rows let fewer waves per value hold a value's rows (headline: 5 -> 4 waves; configs[0]'s
+        // single wave only pays for the copy passes, +8 us per 65,536 adds)
+        A.top1 = cntX >= 2 && maxb % 32 == 0 && waves(cntX - 1) < waves(cntX);
+        A.wpv = waves(cntX - A.top1);
         const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
         // (+ 2 bpw: with dAB / dP, stage_ab's bound / offset tables; a wave's range is at most 64 bits)
         if (bpw > 64) return HM_ERR_UNSUPPORTED;

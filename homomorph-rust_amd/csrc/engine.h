@@ -43,6 +43,8 @@ struct AddArgs {
     uint64_t ws_stride;               // words per value
     uint32_t cntA, cntB, cntAB, cntP; // slot sizes in words (cntA = 2*max cap of a, ...)
     uint32_t cntX;                    // words of x_i = a_i ^ b_i (masked at the degrees)
+    uint32_t top1;                    // prep: word cntX - 1 of every a_i, b_i, x_i is 0 or 1 (the
+                                      // bounds' maximum is a multiple of 32): no product rows for it
     uint32_t wpv;                     // prep: waves per value (bits are dealt round-robin)
     uint32_t prep_lds;                // prep: LDS words per wave
     uint32_t chain_lds;               // chain: LDS words per wave

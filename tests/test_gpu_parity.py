@@ -299,6 +299,41 @@ def test_add_skewed_bounds(H, oracle, chain, skew):
     assert np.array_equal(dec, rdec)
 
 
+@pytest.mark.parametrize("skew", ["uniform", "per_bit"])
+def test_add_prep_top_word_copies(H, oracle, skew):
+    """The prep's top-word copies (AddArgs.top1): when every input bound is at most a multiple of
+    32 (here 256, 288 or 320 per bit and operand) and shorter rows save waves per value, the
+    multiplier words that hold only that bit are added as shifted copies instead of product rows.
+    A batch of 4096 takes that path (4 waves per value) and a batch of 1024 does not (8 waves per
+    value, top1 off): the first 1024 sums must be identical bit for bit, and 16 values equal the
+    oracle's."""
+    params = (128, 128, 1, 128)
+    ctx = make_ctx(H, params, 161)
+    sk, pk, _ = keys(*params, 161)
+    rng = np.random.default_rng(162)
+    if skew == "uniform":
+        ba = bb = np.full(32, 256, dtype=np.uint32)
+    else:
+        ba = rng.choice([256, 288, 320], size=32).astype(np.uint32)
+        bb = rng.choice([256, 288, 320], size=32).astype(np.uint32)
+    n, m = 4096, 1024
+    a, b = plain(n, np.uint32, 163), plain(n, np.uint32, 164)
+    ma, mb = masks(n, 32, 128, 165), masks(n, 32, 128, 166)
+    ca, cb = ctx.encrypt(a, masks=ma, bound=ba), ctx.encrypt(b, masks=mb, bound=bb)
+    big = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    small = ctx.apply2(H.HomomorphicAddition, H.value_slice(ca, 0, m), H.value_slice(cb, 0, m))
+    ctx.synchronize()
+    gl, gd = H.value_slice(big, 0, m).to_host()
+    sl, sd = small.to_host()
+    assert_batches_equal(gl, gd, sl, sd, big.bound, m, f"top-word copies ({skew}) vs product rows")
+    k = 16
+    la, da = oracle.encrypt_batch(pk, as_bytes(a[:k]), ma[:k], ba)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b[:k]), mb[:k], bb)
+    rl, rd = oracle.add_batch(la, da, ba, lb, db, bb, 32, k, big.bound)
+    gl, gd = H.value_slice(big, 0, k).to_host()
+    assert_batches_equal(gl, gd, rl, rd, big.bound, k, f"top-word copies ({skew}) vs oracle")
+
+
 @pytest.mark.parametrize("n", [2048, 2051])
 def test_add_pipeline_same_bits(H, n):
     """hm_ctx_set_add_pipeline: an add as two stream-pipelined halves writes the same ciphertexts
