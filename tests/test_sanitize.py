@@ -6,6 +6,8 @@ engine library's host code, run on the CPU (GPU sanitizers are not available on 
 - tests/sanitize/capi_san.cpp: every host-only C-ABI entry point (status strings, bounds, the
   multiplier cost model, strides, the wire-format parser under 20k corrupted headers, NULL
   contexts), with the device kernels linked in unsanitised;
+- tests/sanitize/plan_split.cpp: the multiplier planner's split Karatsuba plans (host only): the
+  same leaf products as the breadth-first plans at K = 16, K = 21 planned;
 - tests/sanitize/capi_oom.cpp (not sanitised): every allocation inside the multiplier's plan
   builder failed in turn, each call returning HM_ERR_OUT_OF_MEMORY instead of throwing across
   the C ABI.
@@ -50,3 +52,7 @@ def test_engine_host_code_under_asan_ubsan(built):
 def test_engine_abi_returns_oom_instead_of_throwing(built):
     out = _run(os.path.join(built, "capi_oom"))
     assert "ok" in out and "allocation points" in out
+
+
+def test_split_karatsuba_plans_under_asan_ubsan(built):
+    assert "ok" in _run(os.path.join(built, "plan_split"))
