@@ -60,6 +60,8 @@ int main() {
     CHECK(hm_fresh_bound(nullptr) == 0 && hm_ctx_mask_bytes(nullptr) == 0);
     CHECK(hm_ctx_generation(nullptr) == 0 && hm_ctx_stream(nullptr) == nullptr);
     CHECK(hm_add_batch(nullptr, nullptr, nullptr, nullptr) != HM_OK);
+    CHECK(hm_ctx_set_mul_scratch(nullptr, 1000) == HM_ERR_INVALID_ARGUMENT);
+    CHECK(hm_ctx_clear_kernel_timing(nullptr) == HM_ERR_INVALID_ARGUMENT);
     CHECK(hm_wire_encode(nullptr, nullptr, nullptr, 0) != HM_OK);
     CHECK(hm_wire_decode(nullptr, img.data(), img.size(), nullptr) != HM_OK);
     hm_ctx_destroy(nullptr);
