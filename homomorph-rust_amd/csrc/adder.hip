@@ -60,12 +60,14 @@ __device__ __forceinline__ uint64_t checked_limb(uint64_t v, uint32_t d, uint32_
 // the last pass turns them into word counts.  tb: 4 nb LDS words for both ranges' bounds and limb
 // end offsets -- the per-lane bit cursors read them there, never from the by-value Bounds
 // (dev_common.h: by-value argument arrays).  pa/da, pb/db: the value's first limb / degree word.
+// bmask: L - 1 when the range spans several whole values (L a power of two; consecutive values'
+// limbs and degree words are contiguous), so slot t is bit t & bmask.
 __device__ __forceinline__ void stage_ab(const uint64_t *__restrict__ pa, const uint32_t *__restrict__ da,
                                          const Bounds &BA, const uint64_t *__restrict__ pb,
                                          const uint32_t *__restrict__ db, const Bounds &BB, uint32_t i0,
                                          uint32_t nb, uint32_t *Al, uint32_t cntA, uint32_t *nAl,
                                          uint32_t *Bl, uint32_t cntB, uint32_t *nBl, uint32_t *tb,
-                                         int *status) {
+                                         int *status, uint32_t bmask = ~0u) {
     const uint32_t lane = (uint32_t)lane_id();
     i0 = rfl(i0), nb = rfl(nb);
     pa += limb_off(BA, i0), pb += limb_off(BB, i0);
@@ -75,7 +77,8 @@ __device__ __forceinline__ void stage_ab(const uint64_t *__restrict__ pa, const 
     // uniform pass: bounds and inclusive limb end offsets of both ranges, scalar reads only
     uint32_t tota = 0, totb = 0, vba = 0, vea = 0, vbb = 0, veb = 0;
     for (uint32_t t = 0; t < nb; ++t) {
-        const uint32_t ba = BA.b[i0 + t], bb = BB.b[i0 + t];
+        const uint32_t j = (i0 + t) & bmask; // (bmask = L - 1: several whole values per wave)
+        const uint32_t ba = BA.b[j], bb = BB.b[j];
         tota += cap_of(ba), totb += cap_of(bb);
         if (lane == t) vba = ba, vea = tota, vbb = bb, veb = totb;
     }
@@ -119,45 +122,65 @@ __device__ __forceinline__ void stage_ab(const uint64_t *__restrict__ pa, const 
 // (clmul_row_xor_fixed: unrolled, zero-padded); 0: lengths from the degrees
 // TOP1: AddArgs.top1 (the top-word copies below), a separate instance so that the plain one keeps
 // its code (the copies' dead branch cost configs[0]'s prep 1.3 % as a runtime flag)
-template <int NB, int NAB, bool TOP1 = false>
+// MULTI: AddArgs.vpw > 1 -- a wave holds vpw whole values (L = 2^lgL bits each; configs[0]'s
+// one-wave-per-value prep paid a per-wave cost, not a per-bit one): slot t is bit t & (L - 1) of
+// value e + (t >> lgL), and the last bit of every value has no product.
+template <int NB, int NAB, bool TOP1 = false, bool MULTI = false>
 __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     extern __shared__ uint32_t lds[];
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    const uint64_t e = gw / A.wpv;
-    const uint32_t part = (uint32_t)(gw % A.wpv);
-    if (e >= A.n) return;
     const int lane = lane_id();
     const uint32_t L = A.nbits;
-    const uint32_t bpw = (L + A.wpv - 1) / A.wpv; // bit slots per wave: bits [i0, i0 + nmine)
-    const uint32_t i0 = min(L, part * bpw), nmine = min(L, i0 + bpw) - i0;
+    uint64_t e;
+    uint32_t bpw, i0, nmine; // bit slots per wave; this wave's: slots [0, nmine) = bits [i0, i0 + nmine)
+    if constexpr (MULTI) {
+        e = gw * A.vpw;
+        if (e >= A.n) return;
+        bpw = A.vpw * L;
+        i0 = 0;
+        nmine = (uint32_t)min((uint64_t)A.vpw, A.n - e) * L;
+    } else {
+        e = gw / A.wpv;
+        const uint32_t part = (uint32_t)(gw % A.wpv);
+        if (e >= A.n) return;
+        bpw = (L + A.wpv - 1) / A.wpv;
+        i0 = min(L, part * bpw), nmine = min(L, i0 + bpw) - i0;
+    }
+    // slot t's value (relative to e) and bit
+    auto val_of = [&](uint32_t t) -> uint32_t { return MULTI ? t >> A.lgL : 0u; };
+    auto bit_of = [&](uint32_t t) -> uint32_t { return MULTI ? t & (L - 1) : i0 + t; };
     // LDS: [a: bpw cntA][b: bpw cntB][x: bpw cntX][ab: bpw cntAB][P: bpw cntP][na nb dAB dP]
     //      [2 bpw more: with dAB / dP (zeroed after it), stage_ab's bound / end-offset tables]
     uint32_t *Ls = lds + (size_t)wave * A.prep_lds;
     uint32_t *Al = Ls, *Bl = Al + bpw * A.cntA, *Xl = Bl + bpw * A.cntB;
     uint32_t *ABl = Xl + bpw * A.cntX, *Pl = ABl + bpw * A.cntAB;
     uint32_t *nAl = Pl + bpw * A.cntP, *nBl = nAl + bpw, *dAB = nBl + bpw, *dP = dAB + bpw;
+    // a value's workspace: [ab: L cntAB][P: L cntP][deg ab: L][deg P: L][x: L cntX]
+    const size_t oP = (size_t)L * A.cntAB, oDA = oP + (size_t)L * A.cntP, oDP = oDA + L, oX = oDP + L;
     uint32_t *ws = A.ws + e * A.ws_stride;
-    uint32_t *ABg = ws, *Pg = ws + (size_t)L * A.cntAB;
-    uint32_t *degABg = Pg + (size_t)L * A.cntP, *degPg = degABg + L, *Xg = degPg + L;
+    auto wsv = [&](uint32_t t) { return MULTI ? ws + (size_t)val_of(t) * A.ws_stride : ws; };
     const uint64_t *pa = A.a.limbs + e * A.a.stride, *pb = A.b.limbs + e * A.b.stride;
     const uint32_t *da = A.a.degree + e * L, *db = A.b.degree + e * L;
 
     // stage + validate this wave's bits (every bit is validated, the last one too)
-    stage_ab(pa, da, A.ab, pb, db, A.bb, i0, nmine, Al, A.cntA, nAl, Bl, A.cntB, nBl, dAB, A.status);
+    stage_ab(pa, da, A.ab, pb, db, A.bb, i0, nmine, Al, A.cntA, nAl, Bl, A.cntB, nBl, dAB, A.status,
+             MULTI ? L - 1 : ~0u);
     for (uint32_t k = lane; k < 2 * bpw; k += kWave) dAB[k] = 0u;
     wsync();
-    // products only for bits < L-1 (the last bit has no outgoing carry)
-    const uint32_t nprod = min(nmine, (L - 1) - min(i0, L - 1));
+    // products only for bits < L-1 (the last bit has no outgoing carry): slots [0, nprod) with
+    // has_prod (MULTI: every value's last slot skipped)
+    const uint32_t nprod = MULTI ? nmine : min(nmine, (L - 1) - min(i0, L - 1));
+    auto has_prod = [&](uint32_t t) { return !MULTI || bit_of(t) + 1 < L; };
 
     // x_i = a_i ^ b_i for every bit: LDS for the P products, workspace for the chain's sum bits
     for (uint32_t f = lane; f < nmine * A.cntX; f += kWave) {
-        const uint32_t t = f / A.cntX, m = f % A.cntX, i = i0 + t;
+        const uint32_t t = f / A.cntX, m = f % A.cntX, i = bit_of(t);
         const int na = (int)nAl[t], nb = (int)nBl[t];
         const uint32_t x = ((int)m < na ? Al[t * A.cntA + m] : 0u) ^
                            ((int)m < nb ? Bl[t * A.cntB + m] : 0u);
         Xl[t * A.cntX + m] = x;
-        Xg[(size_t)i * A.cntX + m] = x;
+        wsv(t)[oX + (size_t)i * A.cntX + m] = x;
     }
 
     // Products by rows: lanes over (slot t, multiplier word q) -- every lane of a slot runs the
@@ -173,7 +196,8 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
         const uint32_t dt = kWave / cnt, dk = kWave % cnt;
         uint32_t t = (uint32_t)lane / cnt, k = (uint32_t)lane % cnt;
         for (uint32_t f0 = 0; f0 < nprod * cnt; f0 += kWave) {
-            if (t < nprod && k < len(t) && set(t)) atomicXor(&dst[t * dcnt + qt + k], src[t * scnt + k]);
+            if (t < nprod && has_prod(t) && k < len(t) && set(t))
+                atomicXor(&dst[t * dcnt + qt + k], src[t * scnt + k]);
             t += dt, k += dk;
             if (k >= cnt) k -= cnt, ++t;
         }
@@ -182,7 +206,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
         const uint32_t dt = kWave / cq, dq = kWave % cq;
         uint32_t t = (uint32_t)lane / cq, q = (uint32_t)lane % cq;
         for (uint32_t f0 = 0; f0 < nprod * cq; f0 += kWave) {
-            if (t < nprod) row(t, q);
+            if (t < nprod && has_prod(t)) row(t, q);
             t += dt, q += dq;
             if (q >= cq) q -= cq, ++t;
         }
@@ -207,7 +231,7 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     for (uint32_t f = lane; f < nprod * A.cntAB; f += kWave) {
         const uint32_t t = f / A.cntAB, m = f % A.cntAB;
         const uint32_t w = ABl[f];
-        ABg[(size_t)(i0 + t) * A.cntAB + m] = w;
+        if (has_prod(t)) wsv(t)[(size_t)bit_of(t) * A.cntAB + m] = w;
         if (w) atomicMax(&dAB[t], m * 32 + 32 - __builtin_clz(w));
     }
     wsync();
@@ -230,14 +254,15 @@ __global__ void __launch_bounds__(256) add_prep_kernel(AddArgs A) {
     for (uint32_t f = lane; f < nprod * A.cntP; f += kWave) {
         const uint32_t t = f / A.cntP, m = f % A.cntP;
         const uint32_t w = Pl[f] ^ (m < A.cntX ? Xl[t * A.cntX + m] : 0u);
-        Pg[(size_t)(i0 + t) * A.cntP + m] = w;
+        if (has_prod(t)) wsv(t)[oP + (size_t)bit_of(t) * A.cntP + m] = w;
         if (w) atomicMax(&dP[t], m * 32 + 32 - __builtin_clz(w));
     }
     wsync();
     for (uint32_t t = lane; t < nprod; t += kWave) {
-        const uint32_t i = i0 + t;
-        degABg[i] = dAB[t];
-        degPg[i] = dP[t];
+        if (!has_prod(t)) continue;
+        const uint32_t i = bit_of(t);
+        wsv(t)[oDA + i] = dAB[t];
+        wsv(t)[oDP + i] = dP[t];
     }
 }
 
@@ -373,14 +398,18 @@ __global__ void __launch_bounds__(256) add_chain_staged_kernel(AddArgs A) {
 
 int launch_add_prep(const AddArgs &a, void *stream) {
     if (a.n == 0) return 0;
-    // wpv waves per value, 4 waves per block
-    const uint64_t waves = a.n * a.wpv;
+    // wpv waves per value (or vpw values per wave), 4 waves per block
+    const uint64_t waves = a.vpw > 1 ? (a.n + a.vpw - 1) / a.vpw : a.n * a.wpv;
     const uint64_t blocks = (waves + 3) / 4;
     const size_t lds = (size_t)a.prep_lds * 4 * 4;
 #ifndef HM_PREP_FIXED
 #define HM_PREP_FIXED 0 // (A/B knob) 1: product rows at the slots' fixed lengths (measured neutral, r06)
 #endif
-    if (a.top1)
+    if (a.vpw > 1 && a.top1)
+        hipLaunchKernelGGL((add_prep_kernel<0, 0, true, true>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+    else if (a.vpw > 1)
+        hipLaunchKernelGGL((add_prep_kernel<0, 0, false, true>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
+    else if (a.top1)
         hipLaunchKernelGGL((add_prep_kernel<0, 0, true>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
     else if (HM_PREP_FIXED && a.cntB == 10 && a.cntAB == 17)
         hipLaunchKernelGGL((add_prep_kernel<10, 17>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);

@@ -809,9 +809,22 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
         // add its multiples as shifted copies instead of product rows -- worth it when the shorter
         // rows let fewer waves per value hold a value's rows (headline: 5 -> 4 waves; configs[0]'s
         // single wave only pays for the copy passes, +8 us per 65,536 adds)
-        A.top1 = cntX >= 2 && maxb % 32 == 0 && waves(cntX - 1) < waves(cntX);
+        const bool t1ok = cntX >= 2 && maxb % 32 == 0;
+        A.top1 = t1ok && waves(cntX - 1) < waves(cntX);
         A.wpv = waves(cntX - A.top1);
-        const uint32_t bpw = (L + A.wpv - 1) / A.wpv;
+        // one wave per value already (short values, big batch): several whole values per wave
+        // instead when their rows fit one pass (L a power of two: configs[0]'s u8 add, 2 values
+        // of 8 bits x 4 rows with the top-word copies; its prep cost is per wave)
+        A.vpw = 1, A.lgL = 0;
+        if (A.wpv == 1 && (L & (L - 1)) == 0 && a->n >= 16384) {
+            const uint32_t rows = cntX - (t1ok ? 1u : 0u);
+            const uint32_t v = std::min<uint32_t>(8, 64 / std::max<uint32_t>(1, L * rows));
+            if (v >= 2) {
+                A.vpw = v, A.top1 = t1ok;
+                while ((1u << A.lgL) < L) ++A.lgL;
+            }
+        }
+        const uint32_t bpw = A.vpw > 1 ? A.vpw * L : (L + A.wpv - 1) / A.wpv;
         // (+ 2 bpw: with dAB / dP, stage_ab's bound / offset tables; a wave's range is at most 64 bits)
         if (bpw > 64) return HM_ERR_UNSUPPORTED;
         A.prep_lds = even(bpw * (cntA + cntB + cntX + cntAB + cntP) + 6 * bpw);

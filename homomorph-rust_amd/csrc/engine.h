@@ -46,6 +46,8 @@ struct AddArgs {
     uint32_t top1;                    // prep: word cntX - 1 of every a_i, b_i, x_i is 0 or 1 (the
                                       // bounds' maximum is a multiple of 32): no product rows for it
     uint32_t wpv;                     // prep: waves per value (bits are dealt round-robin)
+    uint32_t vpw;                     // prep: > 1: values per wave instead (whole values, L = 2^lgL)
+    uint32_t lgL;                     // prep: log2 nbits when vpw > 1
     uint32_t prep_lds;                // prep: LDS words per wave
     uint32_t chain_lds;               // chain: LDS words per wave
     uint32_t staged;                  // chain: x, ab, P and degrees staged in LDS, carry in place

@@ -334,6 +334,41 @@ def test_add_prep_top_word_copies(H, oracle, skew):
     assert_batches_equal(gl, gd, rl, rd, big.bound, k, f"top-word copies ({skew}) vs oracle")
 
 
+@pytest.mark.parametrize("params", [(64, 64, 1, 64), (32, 32, 1, 32)])
+def test_add_prep_values_per_wave(H, oracle, params):
+    """The prep with several whole values per wave (AddArgs.vpw: u8 values, a batch of at least
+    16,384; 2 values per wave at d = d' = 64, 4 at 32): the same adds at a batch of 1024 run one
+    value per wave, and the first 1024 sums must be identical bit for bit; 16 values equal the
+    oracle's, and a batch whose last wave holds fewer values (16,387) agrees too."""
+    d, dp, delta, tau = params
+    ctx = make_ctx(H, params, 171)
+    sk, pk, _ = keys(*params, 171)
+    n, m = 16387, 1024
+    a, b = plain(n, np.uint8, 172), plain(n, np.uint8, 173)
+    ma, mb = masks(n, 8, tau, 174), masks(n, 8, tau, 175)
+    ca, cb = ctx.encrypt(a, masks=ma), ctx.encrypt(b, masks=mb)
+    big = ctx.apply2(H.HomomorphicAddition, ca, cb)
+    small = ctx.apply2(H.HomomorphicAddition, H.value_slice(ca, 0, m), H.value_slice(cb, 0, m))
+    tail = ctx.apply2(H.HomomorphicAddition, H.value_slice(ca, n - 3, n), H.value_slice(cb, n - 3, n))
+    dec = ctx.decrypt(big)
+    ctx.synchronize()
+    gl, gd = H.value_slice(big, 0, m).to_host()
+    sl, sd = small.to_host()
+    assert_batches_equal(gl, gd, sl, sd, big.bound, m, f"values per wave {params} vs one per wave")
+    gl, gd = H.value_slice(big, n - 3, n).to_host()
+    tl, td = tail.to_host()
+    assert_batches_equal(gl, gd, tl, td, big.bound, 3, f"values per wave {params}: batch tail")
+    k = 16
+    bound = fresh_bound(d, dp, 8)
+    la, da = oracle.encrypt_batch(pk, as_bytes(a[:k]), ma[:k], bound)
+    lb, db = oracle.encrypt_batch(pk, as_bytes(b[:k]), mb[:k], bound)
+    rl, rd = oracle.add_batch(la, da, bound, lb, db, bound, 8, k, big.bound)
+    gl, gd = H.value_slice(big, 0, k).to_host()
+    assert_batches_equal(gl, gd, rl, rd, big.bound, k, f"values per wave {params} vs oracle")
+    rdec = oracle.decrypt_batch(sk, rl, rd, big.bound, 8, k).reshape(-1)
+    assert np.array_equal(dec[:k], rdec)
+
+
 @pytest.mark.parametrize("n", [2048, 2051])
 def test_add_pipeline_same_bits(H, n):
     """hm_ctx_set_add_pipeline: an add as two stream-pipelined halves writes the same ciphertexts

@@ -78,9 +78,10 @@ __global__ void uniform(Args D) {
 
 
 ZERO_SCRATCH = [
-    "_ZN2hm15add_prep_kernelILi10ELi17ELb0EEEvNS_7AddArgsE",  # (fixed rows at d + d' = 256)
-    "_ZN2hm15add_prep_kernelILi0ELi0ELb0EEEvNS_7AddArgsE",
-    "_ZN2hm15add_prep_kernelILi0ELi0ELb1EEEvNS_7AddArgsE",  # (top-word copies: the bench's)
+    "_ZN2hm15add_prep_kernelILi10ELi17ELb0ELb0EEEvNS_7AddArgsE",  # (fixed rows at d + d' = 256)
+    "_ZN2hm15add_prep_kernelILi0ELi0ELb0ELb0EEEvNS_7AddArgsE",
+    "_ZN2hm15add_prep_kernelILi0ELi0ELb1ELb0EEEvNS_7AddArgsE",  # (top-word copies: the bench's)
+    "_ZN2hm15add_prep_kernelILi0ELi0ELb1ELb1EEEvNS_7AddArgsE",  # (values per wave: configs[0])
     "_ZN2hm14decrypt_kernelENS_7DecArgsE",
     "_ZN2hm19decrypt_bits_kernelENS_7DecArgsE",
     "_ZN2hm16mul_final_kernelENS_12MulFinalArgsE",
