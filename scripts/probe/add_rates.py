@@ -13,8 +13,9 @@ import bench  # noqa: E402
 import homomorph as H  # noqa: E402
 
 
-def leg(params, n, dtype, reps, warm):
+def leg(params, n, dtype, reps, warm, chain="auto"):
     ctx = H.Context(H.Parameters(*params), device="cuda:0")
+    ctx.set_add_options(chain)
     ctx.seed_rng(bench.BENCH_SEED)
     ctx.generate_secret_key()
     ctx.generate_public_key()
@@ -35,3 +36,6 @@ s, k, ok = leg((128, 128, 1, 128), 4096, np.uint32, 20, 5)
 s0, k0, ok0 = leg((64, 64, 1, 64), 65536, np.uint8, 100, 5)
 print(f"{tag} u32: step {s:.1f} us chain {k:.1f} prep~{s - k:.1f} ok {ok} | u8: step {s0:.1f} "
       f"chain {k0:.1f} prep~{s0 - k0:.1f} ok {ok0}", flush=True)
+if os.environ.get("VALU_U8"):  # configs[0] on the VALU chain (hm_ctx_set_add_options), for comparison
+    s1, k1, ok1 = leg((64, 64, 1, 64), 65536, np.uint8, 100, 5, "valu")
+    print(f"{tag} u8 valu chain: step {s1:.1f} us chain {k1:.1f} ok {ok1}", flush=True)
