@@ -73,3 +73,14 @@ def test_bench_two_ranks_run_the_engine():
     assert d["world_size_seen"] == 2 and d["n_gpus"] == 2
     assert d["config"]["batch_per_gpu"] == n // 2
     assert d["verified"] == {"correct_sums": n, "correct_products": n, "of": n}
+
+
+def test_bench_two_ranks_headline_add():
+    """The headline add path (run_add) at world size 2 on one card (gloo): each rank adds its own
+    4096-value shard (weak scaling), the sustained-clock replays run per rank, and rank 0 gathers
+    every sum for the check (the driver's N-GPU runs take this path over RCCL)."""
+    d = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1"], env={"HM_BENCH_BACKEND": "gloo"})
+    assert d["world_size_seen"] == 2 and d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["global_batch"] == 8192 and d["verified"]["of"] == 8192
+    assert d["verified"]["correct_sums"] >= 8192 - 16  # (the scheme's noise aside)
+    assert d["roofline"]["sustained"]["kernel_ms"] > 0
