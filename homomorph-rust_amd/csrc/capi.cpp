@@ -795,22 +795,29 @@ hm_status hm_add_batch(hm_ctx *c, const hm_batch *a, const hm_batch *b, hm_batch
     AddArgs A{};
     A.cntA = cntA, A.cntB = cntB, A.cntAB = cntAB, A.cntP = cntP, A.cntX = cntX;
     // prep: enough waves per value to keep the chip busy, and at least enough that one wave's
-    // product rows (bits x multiplier words) fit its 64 lanes in one pass (bits are dealt in
+    // product rows (bits x multiplier words) fit its 64 lanes in two passes (bits are dealt in
     // contiguous ranges)
     {
         const uint64_t want = (16384 + a->n - 1) / a->n;
+        // (rows_fit: waves per value for one pass of a wave's rows; big batches take two passes
+        // per wave -- half the waves: configs[4]'s prep 7.8 -> 5.7 ms per 131,072 adds, the
+        // headline's 4 waves per value unchanged, since its `want` is 4 already)
         auto waves = [&](uint32_t rows) { // rows: product rows per bit
             const uint64_t rows_fit = (L + std::max<uint32_t>(1, 64 / rows) - 1) /
                                       std::max<uint32_t>(1, 64 / rows);
             return (uint32_t)std::max<uint64_t>(
-                1, std::min<uint64_t>({std::max(want, rows_fit), 8, (uint64_t)L}));
+                1, std::min<uint64_t>({std::max(want, (rows_fit + 1) / 2), 8, (uint64_t)L}));
         };
         // the top word of every a_i, b_i, x_i holds at most bit 32 (cntX - 1) = maxb: the prep can
         // add its multiples as shifted copies instead of product rows -- worth it when the shorter
-        // rows let fewer waves per value hold a value's rows (headline: 5 -> 4 waves; configs[0]'s
-        // single wave only pays for the copy passes, +8 us per 65,536 adds)
+        // rows save waves per value or row passes per wave (waves x passes; the headline: 2 passes
+        // -> 1 at 4 waves; one wave and one pass per value only pays for the copy passes, +8 us
+        // per 65,536 u8 adds)
         const bool t1ok = cntX >= 2 && maxb % 32 == 0;
-        A.top1 = t1ok && waves(cntX - 1) < waves(cntX);
+        // row passes per wave at w waves per value (rows per bit)
+        auto passes = [&](uint32_t w, uint32_t rows) { return (((L + w - 1) / w) * rows + 63) / 64; };
+        const uint32_t w0 = waves(cntX), w1 = t1ok ? waves(cntX - 1) : w0;
+        A.top1 = t1ok && (uint64_t)w1 * passes(w1, cntX - 1) < (uint64_t)w0 * passes(w0, cntX);
         A.wpv = waves(cntX - A.top1);
         // one wave per value already (short values, big batch): several whole values per wave
         // instead when their rows fit one pass (L a power of two: configs[0]'s u8 add, 2 values

@@ -36,6 +36,9 @@ s, k, ok = leg((128, 128, 1, 128), 4096, np.uint32, 20, 5)
 s0, k0, ok0 = leg((64, 64, 1, 64), 65536, np.uint8, 100, 5)
 print(f"{tag} u32: step {s:.1f} us chain {k:.1f} prep~{s - k:.1f} ok {ok} | u8: step {s0:.1f} "
       f"chain {k0:.1f} prep~{s0 - k0:.1f} ok {ok0}", flush=True)
+if os.environ.get("MIXED_ADD"):  # configs[4]'s add (d = dp = tau = 256), one 131,072-value chunk
+    s2, k2, ok2 = leg((256, 256, 1, 256), 131072, np.uint32, 3, 1)
+    print(f"{tag} configs[4] add chunk: step {s2:.1f} us chain {k2:.1f} prep~{s2 - k2:.1f} ok {ok2}", flush=True)
 if os.environ.get("VALU_U8"):  # configs[0] on the VALU chain (hm_ctx_set_add_options), for comparison
     s1, k1, ok1 = leg((64, 64, 1, 64), 65536, np.uint8, 100, 5, "valu")
     print(f"{tag} u8 valu chain: step {s1:.1f} us chain {k1:.1f} ok {ok1}", flush=True)

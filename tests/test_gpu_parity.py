@@ -301,12 +301,13 @@ def test_add_skewed_bounds(H, oracle, chain, skew):
 
 @pytest.mark.parametrize("skew", ["uniform", "per_bit"])
 def test_add_prep_top_word_copies(H, oracle, skew):
-    """The prep's top-word copies (AddArgs.top1): when every input bound is at most a multiple of
-    32 (here 256, 288 or 320 per bit and operand) and shorter rows save waves per value, the
-    multiplier words that hold only that bit are added as shifted copies instead of product rows.
-    A batch of 4096 takes that path (4 waves per value) and a batch of 1024 does not (8 waves per
-    value, top1 off): the first 1024 sums must be identical bit for bit, and 16 values equal the
-    oracle's."""
+    """The prep's top-word copies (AddArgs.top1): when the largest input bound is a multiple of 32
+    and shorter rows save waves or row passes, the multiplier words that hold only that bit are
+    added as shifted copies instead of product rows.  Uniform bounds of 256: a batch of 4096
+    takes that path (4 waves per value, one pass) and a batch of 1024 does not (8 waves per
+    value): the first 1024 sums must be identical bit for bit, and 16 values equal the oracle's.
+    Per-bit bounds of 256, 288 or 320 check the same batch split where the host's choice
+    differs (fresh ciphertexts never set those top words)."""
     params = (128, 128, 1, 128)
     ctx = make_ctx(H, params, 161)
     sk, pk, _ = keys(*params, 161)
